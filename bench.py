@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""bench.py -- rANS O0 encode+decode throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 256 MiB of uniform-random bytes per GPU,
+coded as 64 independent 4 MiB buffers, each a reference rANS stream set with
+4096-way lane-interleaved streams (rans::ParallelVariant N = 4096). One step =
+histogram -> [RCCL all-reduce of the 256-bin histogram when N > 1: the shared
+frequency table] -> Rans64Encoder::new on device -> encode -> decode, all
+device-resident. value = uncompressed bytes of all ranks / (t_enc + t_dec).
+
+    python bench.py --gpus 1 --steps 10 --warmup 3
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--buffers", type=int, default=64)
+    p.add_argument("--buffer-mib", type=int, default=4)
+    p.add_argument("--streams", type=int, default=4096)
+    p.add_argument("--kind", default="u")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    return p.parse_args()
+
+
+def cpu_baseline(data, n, B, N, threads):
+    """The oracle (C restatement of src/entropy/rans.rs, 'port') on host cores:
+    Rans64Encoder::new + encode + decode per buffer, buffers spread over threads."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import concurrent.futures as cf
+    import oracle_ffi as O
+    O.lib()
+    nb = min(B, 4 * threads)  # bounded sample: up to 4 buffers per thread
+
+    def one(b):
+        d = data[b * n:(b + 1) * n]
+        t = _table_fast(O, d)
+        enc = O.rans_encode(t, N, d)
+        dec = O.rans_decode(t, N, enc, n)
+        assert dec == d
+        return len(enc)
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(one, range(nb)))
+    dt = time.perf_counter() - t0
+    gib = nb * n / 2**30
+    return {"value": round(gib / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{nb} x {n >> 20} MiB buffers (of the same uniform workload), "
+                      f"histogram+Rans64Encoder::new+encode+decode, x{N} streams, "
+                      f"{threads} threads over buffers, {dt:.2f} s"}
+
+
+def _table_fast(O, d):
+    import numpy as np
+    h = np.bincount(np.frombuffer(d, dtype=np.uint8), minlength=256).astype(np.uint32)
+    return O.rans_table([int(x) for x in h])
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import zipora_amd as zr
+    from zipora_amd.device import RansDeviceBatch
+    L = zr.load()
+    L.zr_set_device(local)
+
+    B, n, N = args.buffers, args.buffer_mib << 20, args.streams
+    total = B * n
+    host = zr.synth(args.kind, total, seed=0x9E3779B97F4A7C15 + rank)
+    raw = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+    bt = RansDeviceBatch([n] * B, N, device=dev, shared_table=True)
+    enc = bt.new_enc()
+    out = bt.new_raw()
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        bt.histogram(raw, stream)
+        if world > 1:  # the shared frequency table: RCCL all-reduce of 256 counts
+            dist.all_reduce(bt.hist, op=dist.ReduceOp.SUM)
+        bt.tables_from_hist(stream)
+        bt.encode(raw, enc, stream)
+        bt.decode(enc, out, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    bt.raise_on_error()
+    if not torch.equal(out, raw):
+        raise SystemExit("decode mismatch after warmup")
+
+    L.zr_timer_reset()
+    L.zr_timer_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    L.zr_timer_enable(0)
+
+    def kt(name):
+        ms, cnt = ctypes.c_double(0), ctypes.c_uint64(0)
+        L.zr_timer_read(name.encode(), ctypes.byref(ms), ctypes.byref(cnt))
+        return ms.value / max(1, cnt.value), cnt.value
+
+    dec_ms, dec_n = kt("rans_decode")
+    enc_ms, _ = kt("rans_encode")
+    cmp_ms, _ = kt("rans_compact")
+    hist_ms, _ = kt("histogram")
+    L.zr_timer_reset()
+
+    bt.raise_on_error()
+    if not torch.equal(out, raw):
+        raise SystemExit("decode mismatch in timed region")
+    comp_bytes = int(bt.enc_len.sum().item())
+
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    value = world * total * args.steps / dt / 2**30
+
+    # dominant kernel: the fast decode (reads C compressed bytes, writes N_in bytes)
+    dec_bytes = comp_bytes + total
+    achieved = dec_bytes / (dec_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
+
+    res = {
+        "metric": "GiB/s encode+decode (device-resident), rANS O0, 256 MiB, 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (uniform xorshift64 bytes, tests/fse_tests.rs:711-717 generator)",
+        "config": {"workload": f"rANS O0 encode+decode, {total >> 20} MiB uniform bytes per GPU as "
+                               f"{B} x {n >> 20} MiB buffers, {N}-way interleaved streams each, "
+                               f"shared table (histogram all-reduce over ranks)",
+                   "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_dec_xn<false> (rans_decode)",
+                     "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
+        "kernels_ms": {"rans_decode": round(dec_ms, 4), "rans_encode": round(enc_ms, 4),
+                       "rans_compact": round(cmp_ms, 4), "histogram": round(hist_ms, 4)},
+        "compressed_bytes": comp_bytes,
+        "ratio": round(comp_bytes / total, 5),
+    }
+    if rank == 0 and world == 1 and not args.no_host_path:
+        # host-resident path (pinned H2D + encode + decode + D2H): DESIGN.md figure
+        pin = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        pin.copy_(torch.frombuffer(bytearray(host), dtype=torch.uint8))
+        pout = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        torch.cuda.synchronize(dev)
+        reps = max(1, min(3, args.steps))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            raw.copy_(pin, non_blocking=True)
+            step()
+            pout.copy_(out, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        res["host_resident_gibps"] = round(total * reps / (time.perf_counter() - t0) / 2**30, 3)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(host, n, B, N, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+/*
+ * zipora_amd.h -- C ABI of the MI355X-native entropy-coding backend for zipora.
+ *
+ * Drop-in boundary for the reference's src/entropy Rust surface.
+ * The reference has no entropy entry points in its C API (src/ffi/c_api.rs:84-608),
+ * so each function below names the Rust method it replaces; INTEGRATION.md shows
+ * the `extern "C"` block a maintainer adds on the Rust side.
+ *
+ * Conventions copied from src/ffi:
+ *   - int32 status codes mirror CResult (src/ffi/mod.rs:29-58);
+ *   - thread-local last error string (src/ffi/c_api.rs:17-42) and an optional
+ *     error callback (src/ffi/c_api.rs:22);
+ *   - no C++ exception crosses the ABI (the catch_unwind guard of c_api.rs:61-76).
+ * Buffers are caller-owned. Functions without the _dev suffix take HOST memory
+ * and are synchronous (they return the codec status like the Rust Result).
+ * Functions with the _dev suffix take DEVICE memory, are ordered on the given
+ * HIP stream (hipStream_t passed as void*, NULL = default stream) and report
+ * per-buffer status into a device int32 array; read it after synchronising.
+ */
+#ifndef ZIPORA_AMD_H
+#define ZIPORA_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (src/ffi/mod.rs:29-58) ---- */
+#define ZR_OK 0
+#define ZR_INVALID_INPUT (-1) /* ZiporaError::InvalidData / InvalidParameter (error.rs:139) */
+#define ZR_MEMORY_ERROR (-2)
+#define ZR_UNSUPPORTED (-4)
+#define ZR_INTERNAL (-5)
+
+typedef void (*zr_error_cb)(int32_t code, const char *message);
+
+const char *zr_last_error(void);               /* c_api.rs:17-42 */
+void zr_set_error_callback(zr_error_cb cb);    /* c_api.rs:22 */
+const char *zr_version(void);
+int32_t zr_device_count(int32_t *count);
+int32_t zr_set_device(int32_t device);         /* binds this host thread to a GPU */
+
+/* ======================================================================
+ * rANS order-0 -- src/entropy/rans.rs
+ * ====================================================================== */
+typedef struct {
+    uint32_t freq[256];  /* normalised frequencies (sum 4096) -- Rans64Symbol::freq */
+    uint32_t start[256]; /* cumulative starts -- Rans64Symbol::start */
+    uint32_t total_freq; /* 4096, or 0 for the empty encoder (rans.rs:209-216) */
+} zr_rans_table;
+
+/* Rans64Encoder::<P>::new(&[u32;256]) -> Result<Self>           rans.rs:208-235 */
+int32_t zr_rans_table_build(const uint32_t raw_freq[256], zr_rans_table *out);
+/* upper bound of Rans64Encoder::encode output for n bytes and P::N = n_streams */
+size_t zr_rans_encode_bound(size_t n, uint32_t n_streams);
+/* Rans64Encoder::<P>::encode(&self, &[u8]) -> Result<Vec<u8>>    rans.rs:338-420
+ * P::N is the runtime n_streams (rans::ParallelVariant::N, rans.rs:165-168). */
+int32_t zr_rans_encode(const zr_rans_table *t, uint32_t n_streams, const uint8_t *in, size_t n,
+                       uint8_t *out, size_t out_cap, size_t *out_len);
+/* Rans64Decoder::<P>::new(&enc).decode(&self, &[u8], usize)      rans.rs:449-651 */
+int32_t zr_rans_decode(const zr_rans_table *t, uint32_t n_streams, const uint8_t *in,
+                       size_t in_len, uint8_t *out, size_t n);
+
+/* ---- device-resident batch pipeline (the GPU hot path) ----
+ * A batch is B independent buffers, each coded as one reference rANS stream
+ * set with P::N = n_streams. Every array below is DEVICE memory.
+ *   raw_off[b], len[b] : buffer b's raw bytes live at raw + raw_off[b], len[b] bytes
+ *   enc_off[b]         : buffer b's encoded bytes live at enc + enc_off[b]
+ *   enc_len[b]         : encoded length (written by encode, read by decode)
+ *   status[b]          : ZR_OK or ZR_INVALID_INPUT (written by both)
+ * Tables are device tables (zr_rans_dtab_bytes() each); table_stride is 0 when
+ * every buffer shares table 0, 1 when buffer b uses table b. */
+typedef struct {
+    uint32_t n_buffers;
+    uint32_t n_streams;
+    uint64_t max_len;        /* >= every len[b]; sizes scratch and grids */
+    const uint64_t *len;
+    const uint64_t *raw_off;
+    const uint64_t *enc_off;
+    uint64_t *enc_len;
+    int32_t *status;
+    const void *tables;
+    uint32_t table_stride;
+} zr_rans_batch;
+
+size_t zr_rans_dtab_bytes(void);
+/* upload host tables (Rans64Encoder::new results) as device tables */
+int32_t zr_rans_dtab_upload(const zr_rans_table *tables, uint32_t n_tables, void *dtabs_dev,
+                            void *stream);
+/* device histograms: per buffer (shared = 0, hist_dev has B x 256 u32) or one
+ * histogram of the whole batch (shared = 1). Accumulates: zero hist_dev first
+ * (zr_memset_dev). The callers this replaces count bytes on the CPU:
+ * RansCompressor::new (compression/mod.rs:433-450), RansBlobStore::train
+ * (blob_store/entropy.rs:212-219), AdaptiveRans64Encoder (rans.rs:708-714). */
+int32_t zr_histogram_dev(const uint8_t *raw, const zr_rans_batch *batch, int32_t shared,
+                         uint32_t *hist_dev, void *stream);
+/* Rans64Encoder::new on device, one table per histogram (no host round trip) */
+int32_t zr_rans_dtab_from_hist_dev(const uint32_t *hist_dev, uint32_t n_tables, void *dtabs_dev,
+                                   void *stream);
+/* bytes of device workspace needed by encode/decode of this batch geometry */
+size_t zr_rans_workspace_bytes(uint32_t n_buffers, uint32_t n_streams, uint64_t max_len);
+/* batched Rans64Encoder::encode: raw -> enc (enc + enc_off[b] must hold
+ * zr_rans_encode_bound(len[b], n_streams) bytes) */
+int32_t zr_rans_encode_batch_dev(const zr_rans_batch *batch, const uint8_t *raw, uint8_t *enc,
+                                 void *workspace, size_t workspace_bytes, void *stream);
+/* batched Rans64Decoder::decode: enc -> raw */
+int32_t zr_rans_decode_batch_dev(const zr_rans_batch *batch, const uint8_t *enc, uint8_t *raw,
+                                 void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---- device memory helpers (for hosts without a HIP binding) ---- */
+int32_t zr_malloc_dev(void **ptr, size_t bytes);
+int32_t zr_free_dev(void *ptr);
+int32_t zr_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
+int32_t zr_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int32_t zr_memset_dev(void *dst, int value, size_t bytes, void *stream);
+int32_t zr_stream_sync(void *stream);
+
+/* ---- kernel timers: HIP events recorded around every launch of the named
+ * kernel on the stream it is launched on ("rans_decode", "rans_encode",
+ * "fse_decode", ...). read() synchronises those events. */
+int32_t zr_timer_enable(int32_t on);
+int32_t zr_timer_reset(void);
+int32_t zr_timer_read(const char *kernel, double *total_ms, uint64_t *launches);
+
+/* ---- synthetic inputs used by bench.py ----
+ * kind 0 'u': xorshift64 bytes (tests/fse_tests.rs:711-717), byte = x >> 32
+ * kind 1 'z': Zipf(alpha = 1.1) over 256 ranks, rank k -> byte k-1
+ * kind 2 't': text-like order-1 Markov bytes over 64 printable symbols */
+int32_t zr_synth_fill(int32_t kind, uint64_t seed, uint8_t *out, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,248 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) -- TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+The oracle restates infinilabs/zipora src/entropy (see oracle/zr_oracle.c).
+"""
+import ctypes
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+_LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+sz = ctypes.c_size_t
+
+
+class RansTable(ctypes.Structure):
+    _fields_ = [("freq", ctypes.c_uint32 * 256), ("start", ctypes.c_uint32 * 256),
+                ("total_freq", ctypes.c_uint32)]
+
+
+class FseConfig(ctypes.Structure):
+    _fields_ = [("table_log", ctypes.c_uint32), ("compression_level", ctypes.c_int32),
+                ("max_table_size", ctypes.c_uint64), ("parallel_blocks", ctypes.c_uint64),
+                ("block_size", ctypes.c_uint64), ("adaptive", ctypes.c_int32)]
+
+
+class HuffTree(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("n_symbols", ctypes.c_int32),
+                ("max_code_length", ctypes.c_uint32), ("code_len", ctypes.c_uint8 * 256),
+                ("code", ctypes.c_uint64 * 256), ("n_nodes", ctypes.c_int32),
+                ("node_leaf", ctypes.c_uint8 * 1024), ("node_sym", ctypes.c_uint8 * 1024),
+                ("node_child", (ctypes.c_int16 * 2) * 1024)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
+                os.path.join(ORACLE_DIR, "zr_oracle.c")):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.or_rans_table_build.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(RansTable)]
+        L.or_rans_encode_bound.argtypes = [sz, ctypes.c_uint32]
+        L.or_rans_encode_bound.restype = sz
+        L.or_rans_encode.argtypes = [ctypes.POINTER(RansTable), ctypes.c_uint32, u8p, sz, u8p,
+                                     ctypes.POINTER(sz)]
+        L.or_rans_decode.argtypes = [ctypes.POINTER(RansTable), ctypes.c_uint32, u8p, sz, u8p, sz]
+        L.or_fse_config_default.argtypes = [ctypes.POINTER(FseConfig)]
+        L.or_fse_compress_bound.argtypes = [sz, ctypes.POINTER(FseConfig)]
+        L.or_fse_compress_bound.restype = sz
+        L.or_fse_compress.argtypes = [ctypes.POINTER(FseConfig), u8p, sz, u8p, ctypes.POINTER(sz)]
+        L.or_fse_decompress.argtypes = [u8p, sz, u8p, sz, ctypes.POINTER(sz)]
+        L.or_fse_decompressed_size.argtypes = [u8p, sz, ctypes.POINTER(sz)]
+        L.or_fse_mul_hi.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.or_fse_mul_hi.restype = ctypes.c_uint64
+        L.or_fse_normalize_exact.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32,
+                                             ctypes.POINTER(ctypes.c_uint32)]
+        L.or_huff_tree_build.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(HuffTree)]
+        L.or_huff_encode_bound.argtypes = [ctypes.POINTER(HuffTree), u8p, sz]
+        L.or_huff_encode_bound.restype = sz
+        L.or_huff_encode.argtypes = [ctypes.POINTER(HuffTree), u8p, sz, u8p, ctypes.POINTER(sz)]
+        L.or_huff_decode.argtypes = [ctypes.POINTER(HuffTree), u8p, sz, u8p, sz, ctypes.POINTER(sz)]
+        L.or_ctx_new.argtypes = [u8p, sz, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L.or_ctx_new.restype = ctypes.c_void_p
+        L.or_ctx_free.argtypes = [ctypes.c_void_p]
+        L.or_ctx_order.argtypes = [ctypes.c_void_p]
+        L.or_ctx_encode_bound.argtypes = [ctypes.c_void_p, u8p, sz]
+        L.or_ctx_encode_bound.restype = sz
+        L.or_ctx_encode.argtypes = [ctypes.c_void_p, u8p, sz, u8p, ctypes.POINTER(sz)]
+        L.or_ctx_encode_xn.argtypes = [ctypes.c_void_p, ctypes.c_int, u8p, sz, u8p, ctypes.POINTER(sz)]
+        L.or_ctx_decode.argtypes = [ctypes.c_void_p, u8p, sz, u8p, sz, ctypes.POINTER(sz)]
+        L.or_ctx_decode_xn.argtypes = [ctypes.c_void_p, ctypes.c_int, u8p, sz, u8p, sz,
+                                       ctypes.POINTER(sz)]
+        L.or_gen_uniform.argtypes = [ctypes.c_uint64, u8p, sz]
+        _lib = L
+    return _lib
+
+
+class OracleError(Exception):
+    pass
+
+
+def _buf(data):
+    data = bytes(data)
+    b = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data + b"\0" if not data else data)
+    return b, len(data)
+
+
+def _out(n):
+    return (ctypes.c_uint8 * max(1, n))()
+
+
+def _check(st, what):
+    if st != 0:
+        raise OracleError(f"{what} failed with status {st}")
+
+
+def histogram(data):
+    import numpy as np
+    d = np.frombuffer(bytes(data), dtype=np.uint8)
+    return [int(x) for x in np.bincount(d, minlength=256)]
+
+
+# ---------------------------------------------------------------- rANS
+def rans_table(raw):
+    t = RansTable()
+    arr = (ctypes.c_uint32 * 256)(*raw)
+    _check(lib().or_rans_table_build(arr, ctypes.byref(t)), "rans_table")
+    return t
+
+
+def rans_encode(table, n_streams, data):
+    b, n = _buf(data)
+    cap = lib().or_rans_encode_bound(n, n_streams)
+    out = _out(cap)
+    ol = sz(0)
+    _check(lib().or_rans_encode(ctypes.byref(table), n_streams, b, n, out, ctypes.byref(ol)),
+           "rans_encode")
+    return ctypes.string_at(out, ol.value)
+
+
+def rans_decode(table, n_streams, enc, n):
+    b, ln = _buf(enc)
+    out = _out(n)
+    _check(lib().or_rans_decode(ctypes.byref(table), n_streams, b, ln, out, n), "rans_decode")
+    return ctypes.string_at(out, n)
+
+
+# ---------------------------------------------------------------- FSE
+def fse_config(**kw):
+    c = FseConfig()
+    lib().or_fse_config_default(ctypes.byref(c))
+    for k, v in kw.items():
+        if k == "parallel_blocks" and v is None:
+            v = 0
+        setattr(c, k, v)
+    return c
+
+
+def fse_compress(data, config=None):
+    c = config or fse_config()
+    b, n = _buf(data)
+    out = _out(lib().or_fse_compress_bound(n, ctypes.byref(c)))
+    ol = sz(0)
+    _check(lib().or_fse_compress(ctypes.byref(c), b, n, out, ctypes.byref(ol)), "fse_compress")
+    return ctypes.string_at(out, ol.value)
+
+
+def fse_decompress(data, cap=None):
+    b, n = _buf(data)
+    if cap is None:
+        s = sz(0)
+        st = lib().or_fse_decompressed_size(b, n, ctypes.byref(s))
+        _check(st, "fse_size")
+        cap = s.value
+    out = _out(cap)
+    ol = sz(0)
+    _check(lib().or_fse_decompress(b, n, out, cap, ctypes.byref(ol)), "fse_decompress")
+    return ctypes.string_at(out, ol.value)
+
+
+# ---------------------------------------------------------------- Huffman
+def huff_tree(freq):
+    t = HuffTree()
+    _check(lib().or_huff_tree_build((ctypes.c_uint32 * 256)(*freq), ctypes.byref(t)), "huff_tree")
+    return t
+
+
+def huff_codes(t):
+    """symbol -> code as a '0'/'1' string in emission order."""
+    return {s: "".join("1" if (t.code[s] >> j) & 1 else "0" for j in range(t.code_len[s]))
+            for s in range(256) if t.code_len[s]}
+
+
+def huff_encode(t, data):
+    b, n = _buf(data)
+    out = _out(lib().or_huff_encode_bound(ctypes.byref(t), b, n))
+    ol = sz(0)
+    _check(lib().or_huff_encode(ctypes.byref(t), b, n, out, ctypes.byref(ol)), "huff_encode")
+    return ctypes.string_at(out, ol.value)
+
+
+def huff_decode(t, enc, n):
+    b, ln = _buf(enc)
+    out = _out(n)
+    ol = sz(0)
+    _check(lib().or_huff_decode(ctypes.byref(t), b, ln, out, n, ctypes.byref(ol)), "huff_decode")
+    return ctypes.string_at(out, ol.value)
+
+
+# ---------------------------------------------------------------- contextual
+class Ctx:
+    def __init__(self, train, order):
+        b, n = _buf(train)
+        st = ctypes.c_int(0)
+        self.h = lib().or_ctx_new(b, n, order, ctypes.byref(st))
+        _check(st.value, "ctx_new")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_ctx_free(self.h)
+
+    @property
+    def order(self):
+        return lib().or_ctx_order(self.h)
+
+    def encode(self, data):
+        b, n = _buf(data)
+        out = _out(lib().or_ctx_encode_bound(self.h, b, n))
+        ol = sz(0)
+        _check(lib().or_ctx_encode(self.h, b, n, out, ctypes.byref(ol)), "ctx_encode")
+        return ctypes.string_at(out, ol.value)
+
+    def encode_xn(self, nway, data):
+        b, n = _buf(data)
+        out = _out(lib().or_ctx_encode_bound(self.h, b, n))
+        ol = sz(0)
+        _check(lib().or_ctx_encode_xn(self.h, nway, b, n, out, ctypes.byref(ol)), "ctx_encode_xn")
+        return ctypes.string_at(out, ol.value)
+
+    def decode(self, enc, n):
+        b, ln = _buf(enc)
+        out = _out(n)
+        ol = sz(0)
+        _check(lib().or_ctx_decode(self.h, b, ln, out, n, ctypes.byref(ol)), "ctx_decode")
+        return ctypes.string_at(out, ol.value)
+
+    def decode_xn(self, nway, enc, n):
+        b, ln = _buf(enc)
+        out = _out(n)
+        ol = sz(0)
+        _check(lib().or_ctx_decode_xn(self.h, nway, b, ln, out, n, ctypes.byref(ol)), "ctx_decode_xn")
+        return ctypes.string_at(out, ol.value)
+
+
+def gen_uniform(n, seed=0x9E3779B97F4A7C15):
+    out = _out(n)
+    lib().or_gen_uniform(seed, out, n)
+    return ctypes.string_at(out, n)

@@ -1,0 +1,22 @@
+"""zipora_amd -- MI355X-native (gfx950) entropy-coding backend for zipora's src/entropy.
+
+Host mirror of the reference's Rust surface over the C ABI of libzipora_amd.so
+(include/zipora_amd.h). Every codec call runs hand-written HIP kernels; there is
+no CPU fallback.
+"""
+from ._lib import load, last_error, LIB_PATH  # noqa: F401
+from .errors import ZiporaError  # noqa: F401
+from .rans import (ParallelVariant, ParallelX1, ParallelX2, ParallelX4, ParallelX8,  # noqa: F401
+                   Rans64Decoder, Rans64Encoder, Rans64Symbol, histogram)
+
+__version__ = "0.1.0"
+
+
+def synth(kind, n, seed=0):
+    """Deterministic synthetic bytes: 'u' uniform xorshift, 'z' Zipf(1.1), 't' text-like."""
+    import ctypes
+    k = {"u": 0, "z": 1, "t": 2}[kind]
+    buf = (ctypes.c_uint8 * max(1, n))()
+    from .errors import check
+    check(load().zr_synth_fill(k, seed, buf, n))
+    return bytes(buf[:n])

@@ -1,0 +1,114 @@
+"""ctypes binding of libzipora_amd.so (the C ABI declared in include/zipora_amd.h).
+
+The product path fails loudly when the HIP library is missing: there is no CPU
+fallback anywhere in this package.
+"""
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libzipora_amd.so")
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_sz = ctypes.c_size_t
+c_vp = ctypes.c_void_p
+
+ZR_OK = 0
+ZR_INVALID_INPUT = -1
+ZR_MEMORY_ERROR = -2
+ZR_UNSUPPORTED = -4
+ZR_INTERNAL = -5
+
+
+class RansTable(ctypes.Structure):
+    _fields_ = [("freq", ctypes.c_uint32 * 256), ("start", ctypes.c_uint32 * 256),
+                ("total_freq", ctypes.c_uint32)]
+
+
+class RansBatch(ctypes.Structure):
+    _fields_ = [("n_buffers", ctypes.c_uint32), ("n_streams", ctypes.c_uint32),
+                ("max_len", ctypes.c_uint64), ("len", c_vp), ("raw_off", c_vp),
+                ("enc_off", c_vp), ("enc_len", c_vp), ("status", c_vp), ("tables", c_vp),
+                ("table_stride", ctypes.c_uint32)]
+
+
+class FseConfig(ctypes.Structure):
+    _fields_ = [("table_log", ctypes.c_uint32), ("compression_level", ctypes.c_int32),
+                ("max_table_size", ctypes.c_uint64), ("parallel_blocks", ctypes.c_uint64),
+                ("block_size", ctypes.c_uint64), ("adaptive", ctypes.c_int32)]
+
+
+# (name, restype, argtypes) for every exported symbol; tests check this list
+# against include/zipora_amd.h.
+SIGNATURES = [
+    ("zr_last_error", ctypes.c_char_p, []),
+    ("zr_set_error_callback", None, [c_vp]),
+    ("zr_version", ctypes.c_char_p, []),
+    ("zr_device_count", ctypes.c_int32, [c_i32p]),
+    ("zr_set_device", ctypes.c_int32, [ctypes.c_int32]),
+    ("zr_rans_table_build", ctypes.c_int32, [c_u32p, ctypes.POINTER(RansTable)]),
+    ("zr_rans_encode_bound", c_sz, [c_sz, ctypes.c_uint32]),
+    ("zr_rans_encode", ctypes.c_int32, [ctypes.POINTER(RansTable), ctypes.c_uint32, c_u8p, c_sz,
+                                        c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_rans_decode", ctypes.c_int32, [ctypes.POINTER(RansTable), ctypes.c_uint32, c_u8p, c_sz,
+                                        c_u8p, c_sz]),
+    ("zr_rans_dtab_bytes", c_sz, []),
+    ("zr_rans_dtab_upload", ctypes.c_int32, [ctypes.POINTER(RansTable), ctypes.c_uint32, c_vp, c_vp]),
+    ("zr_histogram_dev", ctypes.c_int32, [c_vp, ctypes.POINTER(RansBatch), ctypes.c_int32, c_vp, c_vp]),
+    ("zr_rans_dtab_from_hist_dev", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp]),
+    ("zr_rans_workspace_bytes", c_sz, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    ("zr_rans_encode_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp, c_sz,
+                                                  c_vp]),
+    ("zr_rans_decode_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp, c_sz,
+                                                  c_vp]),
+    ("zr_malloc_dev", ctypes.c_int32, [ctypes.POINTER(c_vp), c_sz]),
+    ("zr_free_dev", ctypes.c_int32, [c_vp]),
+    ("zr_memcpy_h2d", ctypes.c_int32, [c_vp, c_vp, c_sz, c_vp]),
+    ("zr_memcpy_d2h", ctypes.c_int32, [c_vp, c_vp, c_sz, c_vp]),
+    ("zr_memset_dev", ctypes.c_int32, [c_vp, ctypes.c_int, c_sz, c_vp]),
+    ("zr_stream_sync", ctypes.c_int32, [c_vp]),
+    ("zr_timer_enable", ctypes.c_int32, [ctypes.c_int32]),
+    ("zr_timer_reset", ctypes.c_int32, []),
+    ("zr_timer_read", ctypes.c_int32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_uint64)]),
+    ("zr_synth_fill", ctypes.c_int32, [ctypes.c_int32, ctypes.c_uint64, c_u8p, c_sz]),
+]
+
+_lib = None
+
+
+def load(build_if_missing=True):
+    """Load the HIP library (building it in-tree first if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        # torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's):
+        # load it first so the process holds ONE HIP runtime and torch streams
+        # and allocations are valid handles for this library too.
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        if not build_if_missing:
+            raise RuntimeError(f"zipora_amd: HIP library missing at {LIB_PATH}; run "
+                               "`python -m zipora_amd.build`")
+        from . import build as _b
+        _b.build()
+    L = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(L, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error():
+    m = load().zr_last_error()
+    return m.decode() if m else ""

@@ -1,0 +1,66 @@
+"""Builds libzipora_amd.so in-tree with hipcc for gfx950 (no JIT cache, no pip install).
+
+    python -m zipora_amd.build            # incremental
+    python -m zipora_amd.build --force
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(PKG, "_obj")
+LIB = os.path.join(PKG, "libzipora_amd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("ZR_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["zr_api.cpp", "zr_rans.hip", "zr_fse.hip", "zr_huff.hip"]
+HEADERS = ["zr_internal.h", os.path.join("..", "..", "include", "zipora_amd.h")]
+CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
+          "-Wno-unused-function", "-Wno-unused-variable", "-munsafe-fp-atomics"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _compile(src):
+    s = os.path.join(CSRC, src)
+    o = os.path.join(OBJ, src + ".o")
+    deps = [s] + [os.path.join(CSRC, h) for h in HEADERS]
+    if not _newer(o, deps):
+        return o
+    cmd = [HIPCC] + CFLAGS + ["-x", "hip", "-c", s, "-o", o]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+    return o
+
+
+def build(force=False, verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    if force:
+        for s in srcs:
+            p = os.path.join(OBJ, s + ".o")
+            if os.path.exists(p):
+                os.remove(p)
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(_compile, srcs))
+    if _newer(LIB, objs) or force:
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    if verbose:
+        print(LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

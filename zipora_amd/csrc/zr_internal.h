@@ -1,0 +1,85 @@
+// zr_internal.h -- shared definitions of the MI355X entropy backend (product code).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+
+#include "../../include/zipora_amd.h"
+
+// ---------------------------------------------------------------------------
+// error plumbing (src/ffi/c_api.rs:17-76 conventions)
+// ---------------------------------------------------------------------------
+namespace zr {
+int32_t set_error(int32_t code, const std::string &msg);
+void clear_error();
+
+#define ZR_HIP(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return ::zr::set_error(ZR_INTERNAL, std::string("HIP error: ") +              \
+                                                    hipGetErrorString(e_) + " at " #expr); \
+    } while (0)
+
+#define ZR_GUARD_BEGIN try {
+#define ZR_GUARD_END                                                   \
+    }                                                                  \
+    catch (const std::bad_alloc &) {                                   \
+        return ::zr::set_error(ZR_MEMORY_ERROR, "out of host memory"); \
+    }                                                                  \
+    catch (...) {                                                      \
+        return ::zr::set_error(ZR_INTERNAL, "internal exception");     \
+    }
+
+// ---------------------------------------------------------------------------
+// rANS constants (src/entropy/rans.rs:14-16)
+// ---------------------------------------------------------------------------
+constexpr uint32_t RANS_L = 1u << 16;
+constexpr uint32_t TF_SHIFT = 12;
+constexpr uint32_t TOTFREQ = 1u << TF_SHIFT;
+
+// Device table: everything the encode and decode kernels need for one
+// normalised frequency table. 16-byte aligned, copied into LDS per workgroup.
+enum : uint32_t { DT_NORMAL = 0, DT_SINGLE = 1, DT_EMPTY = 2 };
+struct alignas(16) RansDTab {
+    uint32_t kind;      // DT_NORMAL: every freq <= 4095; DT_SINGLE: one symbol owns 4096; DT_EMPTY
+    uint32_t status;    // ZR_OK, or ZR_INVALID_INPUT if normalisation failed
+    uint32_t pad[2];
+    uint32_t freq[256];
+    uint32_t start[256];
+    // encode: q = umulhi(x << 8, rcp) >> rsh == x / freq for every x < 2^24
+    // (Granlund-Montgomery with N = 24, l = ceil(log2 freq), rcp = ceil(2^(24+l)/freq))
+    uint32_t rcp[256];
+    uint32_t rsh[256];
+    // decode: slot -> sym | (slot - start) << 8 | freq << 20   (freq <= 4095 when DT_NORMAL)
+    uint32_t slot[TOTFREQ];
+};
+
+// host-side Rans64Encoder::new restatement (used by zr_rans_table_build and dtab upload)
+int32_t rans_normalize_host(const uint32_t raw[256], zr_rans_table *out);
+void rans_dtab_from_table(const zr_rans_table *t, RansDTab *d);
+
+// per-batch workspace carve (device pointers)
+struct RansWork {
+    uint32_t *st_state;   // [B*N]
+    uint32_t *st_len;     // [B*N]
+    uint64_t *blocksum;   // [B*nblk]
+    uint64_t *blockoff;   // [B*nblk]
+    uint32_t *redo;       // [B*nblk]
+    uint8_t *scratch;     // [B*R]
+    uint64_t region;      // R: scratch bytes per buffer
+    uint32_t cap;         // scratch bytes per stream (xN mode)
+    uint32_t nblk;
+};
+size_t rans_workspace_bytes(uint32_t B, uint32_t N, uint64_t max_len);
+int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t bytes, RansWork *w);
+
+// HIP-event timing of named kernels (zr_timer_* in the C ABI). When enabled,
+// launchers bracket the named kernel with events recorded on its own stream.
+void timer_begin(const char *name, hipStream_t s);
+void timer_end(const char *name, hipStream_t s);
+
+inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+inline uint64_t round_up(uint64_t a, uint64_t b) { return ceil_div(a, b) * b; }
+}  // namespace zr

@@ -1,0 +1,755 @@
+// zr_rans.hip -- rANS order-0 (src/entropy/rans.rs) on MI355X / gfx950.
+//
+// Layout in HBM (bit-exact with the reference, rans.rs:402-419 / Appendix A):
+//   xN (len >= N > 1): state[0..N]:u64 LE | len[0..N]:u32 LE | stream_0 | ... | stream_{N-1}
+//   x1 (N == 1 or len < N): renorm bytes in emission order | state:u64 LE
+// Stream s holds symbols s, s+N, s+2N, ...; encoded last-to-first, decoded first-to-last
+// reading its bytes backwards.
+//
+// Work decomposition: one lane = one coder state = one stream. A 256-thread
+// workgroup owns 256 consecutive streams of one buffer, so step k of the
+// workgroup touches 256 consecutive bytes raw[k*N + 256*blk ...]: the raw side
+// is staged through an LDS tile and moved with 16-byte coalesced accesses.
+// The decode slot table (16 KiB) and encode symbol table (2 KiB) live in LDS.
+// Per-buffer x1 streams (blob records) run one lane per buffer.
+#include "zr_internal.h"
+
+namespace zr {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t ld_u32_u(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ uint64_t ld_u64_u(const uint8_t *p) {
+    return (uint64_t)ld_u32_u(p) | ((uint64_t)ld_u32_u(p + 4) << 32);
+}
+__device__ __forceinline__ void st_u32_u(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+    p[2] = (uint8_t)(v >> 16);
+    p[3] = (uint8_t)(v >> 24);
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan(unsigned long long v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        unsigned long long t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// exclusive scan over a 256-thread block; sh must hold 4 entries
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, unsigned long long *sh,
+                                                    uint64_t *total) {
+    unsigned long long inc = wave_incl_scan(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) sh[w] = inc;
+    __syncthreads();
+    unsigned long long base = 0;
+    for (int i = 0; i < w; i++) base += sh[i];
+    if (total) *total = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+    return base + inc - v;
+}
+
+__device__ __forceinline__ uint64_t block_sum(uint64_t v, unsigned long long *sh) {
+    uint64_t t;
+    block_excl_scan(v, sh, &t);
+    return t;
+}
+
+__device__ __forceinline__ const RansDTab *tab_for(const void *tables, uint32_t stride, uint32_t b) {
+    return reinterpret_cast<const RansDTab *>(tables) + (size_t)stride * b;
+}
+
+__device__ __forceinline__ bool single_mode(uint64_t n, uint32_t N) { return N <= 1 || n < N; }
+
+struct KArgs {  // kernel-side copy of zr_rans_batch
+    uint32_t B, N;
+    uint64_t max_len;
+    const uint64_t *len, *raw_off, *enc_off;
+    uint64_t *enc_len;
+    int32_t *status;
+    const void *tables;
+    uint32_t table_stride;
+};
+
+// ======================================================================
+// histogram (the callers' [u32;256] counts: compression/mod.rs:433-436,
+// blob_store/entropy.rs:213-216, rans.rs:708-714)
+// ======================================================================
+__global__ __launch_bounds__(256) void k_hist(const uint8_t *raw, KArgs a, int shared,
+                                              uint32_t *hist, uint64_t chunk, uint32_t nchunk) {
+    const uint32_t b = blockIdx.x / nchunk, c = blockIdx.x % nchunk;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    const uint64_t lo = (uint64_t)c * chunk;
+    if (lo >= n) return;
+    const uint64_t hi = min(n, lo + chunk);
+    __shared__ uint32_t h[4][257];
+    for (int i = threadIdx.x; i < 4 * 257; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t *mine = h[threadIdx.x >> 6];
+    const uint8_t *p = raw + a.raw_off[b];
+    // head bytes up to 16-byte alignment
+    const uint64_t mis = (16 - (((uintptr_t)(p + lo)) & 15)) & 15;
+    const uint64_t body_lo = min(hi, lo + mis);
+    if (threadIdx.x < body_lo - lo) atomicAdd(&mine[p[lo + threadIdx.x]], 1u);
+    const uint64_t units = (hi - body_lo) / 16;
+    const uint4 *q = reinterpret_cast<const uint4 *>(p + body_lo);
+    for (uint64_t u = threadIdx.x; u < units; u += 256) {
+        uint4 v = q[u];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            atomicAdd(&mine[w[j] & 0xFF], 1u);
+            atomicAdd(&mine[(w[j] >> 8) & 0xFF], 1u);
+            atomicAdd(&mine[(w[j] >> 16) & 0xFF], 1u);
+            atomicAdd(&mine[w[j] >> 24], 1u);
+        }
+    }
+    const uint64_t tail_lo = body_lo + units * 16;
+    if (threadIdx.x < hi - tail_lo) atomicAdd(&mine[p[tail_lo + threadIdx.x]], 1u);
+    __syncthreads();
+    const uint32_t v = threadIdx.x;
+    const uint32_t s = h[0][v] + h[1][v] + h[2][v] + h[3][v];
+    if (s) atomicAdd(&hist[(shared ? 0 : (size_t)b * 256) + v], s);
+}
+
+// ======================================================================
+// table build on device: Rans64Encoder::new (rans.rs:208-235) with
+// normalize_frequencies (rans.rs:238-299) and the symbol starts (rans.rs:225-228)
+// ======================================================================
+__global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tabs) {
+    __shared__ unsigned long long sh[4];
+    __shared__ uint32_t norm_s[256], start_s[256], freq_raw[256];
+    __shared__ unsigned long long best;
+    const uint32_t v = threadIdx.x;
+    RansDTab *d = tabs + blockIdx.x;
+    const uint32_t f = hist[(size_t)blockIdx.x * 256 + v];
+    freq_raw[v] = f;
+    // total_freq: u32 wrapping sum (rans.rs:209)
+    const uint32_t total = (uint32_t)block_sum(f, sh);
+    if (total == 0) {  // empty encoder (rans.rs:210-216)
+        d->freq[v] = 0;
+        d->start[v] = 0;
+        d->rcp[v] = 0;
+        d->rsh[v] = 0;
+        for (int j = v; j < (int)TOTFREQ; j += 256) d->slot[j] = 0;
+        if (v == 0) {
+            d->kind = DT_EMPTY;
+            d->status = ZR_OK;
+        }
+        return;
+    }
+    // pass 1: one slot per present symbol (rans.rs:244-250)
+    const uint32_t used = (uint32_t)block_sum(f > 0, sh);
+    const uint64_t ir = TOTFREQ - used;  // initial_remaining (rans.rs:263)
+    // pass 2: proportional share of the initial budget (rans.rs:264-271). The
+    // min(remaining) clamp never binds because sum(f*ir/total) <= ir.
+    uint32_t add = f > 0 ? (uint32_t)(((uint64_t)f * ir) / (uint64_t)total) : 0;
+    uint32_t norm = (f > 0 ? 1u : 0u) + add;
+    uint32_t remaining = (uint32_t)(ir - block_sum(add, sh));
+    norm_s[v] = norm;
+    __syncthreads();
+    // pass 3 (rans.rs:274-296): +1 to the largest raw freq (lowest index on ties)
+    // whose normalised freq is < 1024; repeated +1 on the same argmax is batched.
+    while (remaining > 0) {
+        if (v == 0) best = 0;
+        __syncthreads();
+        const uint32_t fv = freq_raw[v];
+        if (fv > 0 && norm_s[v] < TOTFREQ / 4)
+            atomicMax(&best, ((unsigned long long)fv << 8) | (255 - v));
+        __syncthreads();
+        const unsigned long long bk = best;
+        __syncthreads();
+        if (bk == 0) {  // fallback: first non-zero symbol (rans.rs:284-292)
+            if (v == 0) {
+                for (int i = 0; i < 256; i++)
+                    if (freq_raw[i] > 0) {
+                        norm_s[i] += remaining;
+                        break;
+                    }
+            }
+            remaining = 0;
+        } else {
+            const uint32_t idx = 255 - (uint32_t)(bk & 0xFF);
+            const uint32_t give = min(remaining, TOTFREQ / 4 - norm_s[idx]);
+            if (v == 0) norm_s[idx] += give;
+            remaining -= give;
+        }
+        __syncthreads();
+    }
+    norm = norm_s[v];
+    uint64_t tot;
+    const uint32_t start = (uint32_t)block_excl_scan(norm, sh, &tot);
+    start_s[v] = start;
+    d->freq[v] = norm;
+    d->start[v] = start;
+    uint32_t l = norm <= 1 ? 0u : 32u - __clz(norm - 1);
+    d->rsh[v] = l;
+    d->rcp[v] = norm ? (uint32_t)(((1ull << (24 + l)) + norm - 1) / norm) : 0u;
+    const uint32_t maxn = (uint32_t)__syncthreads_or(norm == TOTFREQ);
+    __syncthreads();
+    for (uint32_t j = v; j < TOTFREQ; j += 256) {
+        // owner of slot j: last symbol with start <= j (zero-freq symbols share the next start)
+        int lo = 0, hi = 255;
+        while (lo < hi) {
+            int mid = (lo + hi + 1) >> 1;
+            if (start_s[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint32_t fs = norm_s[lo];
+        d->slot[j] = (uint32_t)lo | ((j - start_s[lo]) << 8) | ((fs < TOTFREQ ? fs : 0u) << 20);
+    }
+    if (v == 0) {
+        d->kind = maxn ? DT_SINGLE : DT_NORMAL;
+        d->status = ZR_OK;
+    }
+}
+
+// ======================================================================
+// encode, xN layout: one lane per stream (rans.rs:369-420, encode_symbol :303-335)
+// ======================================================================
+__global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
+    const uint32_t nblk = w.nblk;
+    const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    const uint32_t N = a.N;
+    if (single_mode(n, N)) return;
+    __shared__ uint2 et[256];  // x: freq | start << 13 ; y: rcp | rsh << 27
+    __shared__ unsigned long long sh[4];
+    const RansDTab *T = tab_for(a.tables, a.table_stride, b);
+    {
+        const uint32_t v = threadIdx.x;
+        et[v] = make_uint2(T->freq[v] | (T->start[v] << 13), T->rcp[v] | (T->rsh[v] << 27));
+    }
+    __syncthreads();
+    const uint32_t s = blk * 256 + threadIdx.x;
+    const bool active = s < N;
+    const uint64_t c = active ? (n - s - 1) / N + 1 : 0;  // symbols s, s+N, ... < n
+    const uint64_t cmax = (n - 1) / N + 1;
+    const uint8_t *in = raw + a.raw_off[b] + s;
+    uint32_t *out = reinterpret_cast<uint32_t *>(w.scratch + (size_t)b * w.region + (size_t)s * w.cap);
+    uint32_t x = RANS_L, acc = 0, nacc = 0, nout = 0;  // nout = dwords stored
+    bool err = false;
+    for (uint64_t k = cmax; k-- > 0;) {
+        if (k < c && !err) {
+            const uint32_t sym = in[k * N];
+            const uint2 e = et[sym];
+            const uint32_t f = e.x & 0x1FFF;
+            if (f == 0) {  // "Symbol {} not in frequency table" (rans.rs:311-316)
+                err = true;
+                continue;
+            }
+            const uint32_t xmax = f << TF_SHIFT;  // ((L << 8) / TOTFREQ) * freq (rans.rs:319)
+#pragma unroll
+            for (int r = 0; r < 2; r++) {  // x < 2^24 and xmax >= 2^12: at most 2 bytes
+                if (x >= xmax) {
+                    acc |= (x & 0xFF) << (8 * nacc);
+                    x >>= 8;
+                    if (++nacc == 4) {
+                        out[nout++] = acc;
+                        acc = 0;
+                        nacc = 0;
+                    }
+                }
+            }
+            const uint32_t q = __umulhi(x << 8, e.y & 0x7FFFFFF) >> (e.y >> 27);  // x / f
+            x = x + (e.x >> 13) + q * (TOTFREQ - f);  // (x/f)*4096 + x%f + start
+        }
+    }
+    if (nacc) out[nout] = acc;
+    if (err) atomicOr(&a.status[b], 1);  // marked; converted to ZR_INVALID_INPUT by the scan
+    const uint32_t bytes = nout * 4 + nacc;
+    if (active) {
+        w.st_state[(size_t)b * N + s] = x;
+        w.st_len[(size_t)b * N + s] = bytes;
+    }
+    const uint64_t bs = block_sum(active ? bytes : 0, sh);
+    if (threadIdx.x == 0) w.blocksum[(size_t)b * nblk + blk] = bs;
+}
+
+// ======================================================================
+// encode/decode, x1 layout: one lane per buffer (encode_single rans.rs:354-366)
+// ======================================================================
+__global__ __launch_bounds__(64) void k_enc_x1(const uint8_t *raw, KArgs a, RansWork w) {
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    if (!single_mode(n, a.N)) return;
+    const RansDTab *T = tab_for(a.tables, a.table_stride, b);
+    const uint8_t *in = raw + a.raw_off[b];
+    uint8_t *out = w.scratch + (size_t)b * w.region;
+    uint32_t x = RANS_L;
+    uint64_t no = 0;
+    bool err = false;
+    for (uint64_t i = n; i-- > 0;) {
+        const uint32_t sym = in[i];
+        const uint32_t f = T->freq[sym];
+        if (f == 0) {
+            err = true;
+            break;
+        }
+        const uint32_t xmax = f << TF_SHIFT;
+        while (x >= xmax) {
+            out[no++] = (uint8_t)x;
+            x >>= 8;
+        }
+        const uint32_t q = __umulhi(x << 8, T->rcp[sym]) >> T->rsh[sym];
+        x = x + T->start[sym] + q * (TOTFREQ - f);
+    }
+    if (err) a.status[b] = ZR_INVALID_INPUT;
+    w.st_state[(size_t)b * a.N] = x;
+    w.blocksum[(size_t)b * w.nblk] = no;  // x1: renorm byte count
+    a.enc_len[b] = no + 8;
+}
+
+// per-buffer exclusive scan of block sums; validates decode headers
+__global__ __launch_bounds__(256) void k_scan(KArgs a, RansWork w, int decode) {
+    const uint32_t b = blockIdx.x;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    const uint32_t N = a.N;
+    if (single_mode(n, N)) return;
+    __shared__ unsigned long long sh[4];
+    const uint32_t nblk = w.nblk;
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < nblk; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        const uint64_t v = i < nblk ? w.blocksum[(size_t)b * nblk + i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan(v, sh, &tot);
+        if (i < nblk) w.blockoff[(size_t)b * nblk + i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        const uint64_t hdr = (uint64_t)N * 12;
+        if (!decode) {
+            a.enc_len[b] = hdr + carry;
+            if (a.status[b] != 0) a.status[b] = ZR_INVALID_INPUT;
+        } else if (a.status[b] == 0 && hdr + carry > a.enc_len[b]) {
+            a.status[b] = ZR_INVALID_INPUT;  // "Invalid stream data length" (rans.rs:608-610)
+        }
+    }
+}
+
+// header + stream compaction of the xN layout (rans.rs:402-419)
+__global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, RansWork w) {
+    const uint32_t nblk = w.nblk;
+    const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    const uint32_t N = a.N;
+    if (single_mode(n, N) || a.status[b] != 0) return;
+    __shared__ unsigned long long sh[4];
+    __shared__ uint64_t soff[256];
+    __shared__ uint32_t slen[256];
+    const uint32_t s = blk * 256 + threadIdx.x;
+    const bool active = s < N;
+    const uint32_t L = active ? w.st_len[(size_t)b * N + s] : 0;
+    const uint64_t off = block_excl_scan(L, sh, nullptr) + w.blockoff[(size_t)b * nblk + blk];
+    soff[threadIdx.x] = off;
+    slen[threadIdx.x] = L;
+    uint8_t *e = enc + a.enc_off[b];
+    if (active) {
+        const uint32_t x = w.st_state[(size_t)b * N + s];
+        st_u32_u(e + 8 * (size_t)s, x);
+        st_u32_u(e + 8 * (size_t)s + 4, 0);
+        st_u32_u(e + 8 * (size_t)N + 4 * (size_t)s, L);
+    }
+    __syncthreads();
+    // each wave copies 64 streams, all lanes on one stream at a time
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t *dbase = e + 12 * (size_t)N;
+    for (int j = wv * 64; j < wv * 64 + 64; j++) {
+        const uint32_t sj = blk * 256 + j;
+        if (sj >= N) break;
+        const uint8_t *src = w.scratch + (size_t)b * w.region + (size_t)sj * w.cap;
+        uint8_t *dst = dbase + soff[j];
+        const uint32_t Lj = slen[j];
+        for (uint32_t i = lane; i < Lj; i += 64) dst[i] = src[i];
+    }
+}
+
+__global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, RansWork w) {
+    const uint32_t b = blockIdx.x;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    if (!single_mode(n, a.N) || a.status[b] != 0) return;
+    const uint64_t L = w.blocksum[(size_t)b * w.nblk];
+    const uint8_t *src = w.scratch + (size_t)b * w.region;
+    uint8_t *dst = enc + a.enc_off[b];
+    for (uint64_t i = threadIdx.x; i < L; i += 64) dst[i] = src[i];
+    if (threadIdx.x < 8) {
+        const uint64_t x = w.st_state[(size_t)b * a.N];
+        dst[L + threadIdx.x] = (uint8_t)(x >> (8 * threadIdx.x));
+    }
+}
+
+// ======================================================================
+// decode
+// ======================================================================
+// block sums of the xN stream lengths read from the encoded header (rans.rs:589-606)
+__global__ __launch_bounds__(256) void k_dec_hdr(const uint8_t *enc, KArgs a, RansWork w) {
+    const uint32_t nblk = w.nblk;
+    const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    const uint32_t N = a.N;
+    if (n == 0 || single_mode(n, N)) return;
+    __shared__ unsigned long long sh[4];
+    const uint64_t hdr = (uint64_t)N * 12;
+    const bool hdr_ok = a.enc_len[b] >= hdr;  // min_header_size (rans.rs:563-568)
+    const uint32_t s = blk * 256 + threadIdx.x;
+    uint64_t L = 0;
+    if (hdr_ok && s < N) L = ld_u32_u(enc + a.enc_off[b] + 8 * (size_t)N + 4 * (size_t)s);
+    const uint64_t bs = block_sum(L, sh);
+    if (threadIdx.x == 0) {
+        w.blocksum[(size_t)b * nblk + blk] = bs;
+        w.redo[(size_t)b * nblk + blk] = 0;
+        if (!hdr_ok && blk == 0) a.status[b] = ZR_INVALID_INPUT;
+    }
+}
+
+constexpr int TILE = 16;  // decode steps staged per LDS tile
+
+// Writes rows [k0, k0+rows) of the staged tile to raw (row k -> raw[k*N + 256*blk ...]).
+__device__ __forceinline__ void flush_tile(const uint8_t *tile, uint8_t *outb, uint64_t n, uint32_t N,
+                                           uint32_t blk, uint64_t k0, uint32_t rows, bool vec_ok) {
+    const uint32_t col0 = blk * 256;
+    const uint32_t width = min(256u, N - col0);
+    if (vec_ok && width == 256) {
+        // 16 threads per row, 16 bytes each
+        const uint32_t r = threadIdx.x >> 4, cc = (threadIdx.x & 15) * 16;
+        if (r < rows) {
+            const uint64_t k = k0 + r;
+            const uint64_t rowbase = k * N + col0;
+            if (rowbase + 256 <= n) {
+                *reinterpret_cast<uint4 *>(outb + rowbase + cc) =
+                    *reinterpret_cast<const uint4 *>(tile + r * 256 + cc);
+            } else {
+                for (uint32_t j = 0; j < 16; j++)
+                    if (rowbase + cc + j < n) outb[rowbase + cc + j] = tile[r * 256 + cc + j];
+            }
+        }
+    } else {
+        const uint32_t t = threadIdx.x;
+        if (t < width) {
+            for (uint32_t r = 0; r < rows; r++) {
+                const uint64_t pos = (k0 + r) * N + col0 + t;
+                if (pos < n) outb[pos] = tile[r * 256 + t];
+            }
+        }
+    }
+}
+
+// Fast path: 32-bit state in [2^16, 2^24), packed LDS slot table, 64-bit MSB-first
+// register window over the stream bytes refilled by aligned dword loads.
+// GENERIC: u64 state, any table kind, byte-wise renormalisation exactly as
+// decode_symbol (rans.rs:472-507). Workgroups the fast path cannot take are
+// flagged in w.redo and re-run by the GENERIC instance.
+template <bool GENERIC>
+__global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w) {
+    const uint32_t nblk = w.nblk;
+    const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    const uint32_t N = a.N;
+    if (n == 0 || single_mode(n, N) || a.status[b] != 0) return;
+    if (GENERIC && !w.redo[(size_t)b * nblk + blk]) return;
+    __shared__ uint32_t stab[TOTFREQ];
+    __shared__ uint8_t tile[TILE * 256];
+    __shared__ unsigned long long sh[4];
+    __shared__ uint32_t gfreq[GENERIC ? 256 : 1], gstart[GENERIC ? 256 : 1];
+    const RansDTab *T = tab_for(a.tables, a.table_stride, b);
+    for (uint32_t j = threadIdx.x; j < TOTFREQ; j += 256) stab[j] = T->slot[j];
+    if (GENERIC) {
+        gfreq[threadIdx.x] = T->freq[threadIdx.x];
+        gstart[threadIdx.x] = T->start[threadIdx.x];
+    }
+    const uint32_t kind = T->kind;
+    const uint32_t s = blk * 256 + threadIdx.x;
+    const bool active = s < N;
+    const uint8_t *e = enc + a.enc_off[b];
+    const uint32_t L = active ? ld_u32_u(e + 8 * (size_t)N + 4 * (size_t)s) : 0;
+    const uint64_t off = block_excl_scan(L, sh, nullptr) + w.blockoff[(size_t)b * nblk + blk];
+    uint64_t X = active ? ld_u64_u(e + 8 * (size_t)s) : RANS_L;
+    if (!GENERIC) {
+        const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24);
+        if (__syncthreads_or(!fast)) {
+            if (threadIdx.x == 0) w.redo[(size_t)b * nblk + blk] = 1;
+            return;
+        }
+    }
+    __syncthreads();
+    const uint64_t c = active ? (n - s - 1) / N + 1 : 0;
+    const uint64_t cmax = (n - 1) / N + 1;
+    const uint8_t *sb = e + 12 * (size_t)N + off;  // stream start
+    uint8_t *outb = raw + a.raw_off[b];
+    const bool vec_ok = ((((uintptr_t)outb) | N) & 15) == 0;
+    bool err = false;
+
+    // ---- fast-path lane state
+    uint32_t x = (uint32_t)X;
+    uint64_t win = 0;
+    uint32_t nbits = 0;
+    uint64_t consumed = 0;  // bits
+    const uintptr_t lo_lim = ((uintptr_t)a.enc_off[b] + (uintptr_t)enc) & ~(uintptr_t)3;
+    uintptr_t rp = 0;
+    // ---- generic lane state
+    uint64_t pos = L;
+
+    if (!GENERIC && active) {
+        const uintptr_t pend = (uintptr_t)sb + L;
+        const uintptr_t a0 = (pend - 1) & ~(uintptr_t)3;
+        const uint32_t v = (uint32_t)(pend - a0);  // 1..4 valid bytes in the first dword
+        const uint32_t w0 = *reinterpret_cast<const uint32_t *>(a0 > lo_lim ? a0 : lo_lim);
+        win = (uint64_t)(w0 << (32 - 8 * v)) << 32;
+        nbits = 8 * v;
+        rp = a0 - 4;
+    }
+
+    for (uint64_t k0 = 0; k0 < cmax; k0 += TILE) {
+        const uint32_t rows = (uint32_t)min((uint64_t)TILE, cmax - k0);
+        for (uint32_t r = 0; r < rows; r++) {
+            const uint64_t k = k0 + r;
+            uint8_t sym = 0;
+            if (k < c) {
+                if (!GENERIC) {
+                    // renormalise before decoding (rans.rs:479-485): x in [16, 2^24) needs
+                    // 0, 1 or 2 bytes: sh = 8 * (#bytes) from the leading-zero count
+                    const uint32_t sh8 = (__clz(x) & 24) - 8;
+                    const uint32_t t = __builtin_amdgcn_ubfe((uint32_t)(win >> 32), 32 - sh8, sh8);
+                    x = (x << sh8) | t;
+                    win <<= sh8;
+                    nbits -= sh8;
+                    consumed += sh8;
+                    if (nbits <= 32) {
+                        const uintptr_t ra = rp > lo_lim ? rp : lo_lim;
+                        const uint32_t ww = *reinterpret_cast<const uint32_t *>(ra);
+                        win |= (uint64_t)ww << (32 - nbits);
+                        nbits += 32;
+                        rp -= 4;
+                    }
+                    const uint32_t ent = stab[x & (TOTFREQ - 1)];
+                    x = __umul24(ent >> 20, x >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
+                    sym = (uint8_t)ent;
+                } else if (!err) {
+                    while (X < RANS_L) {
+                        if (pos == 0) {  // "Insufficient data for decoding" (rans.rs:480-482)
+                            err = true;
+                            break;
+                        }
+                        pos--;
+                        X = (X << 8) | sb[pos];
+                    }
+                    if (!err) {
+                        const uint32_t slot = (uint32_t)(X & (TOTFREQ - 1));
+                        const uint32_t sy = stab[slot] & 0xFF;
+                        X = (uint64_t)gfreq[sy] * (X >> TF_SHIFT) + slot - gstart[sy];
+                        sym = (uint8_t)sy;
+                    }
+                }
+            }
+            tile[r * 256 + threadIdx.x] = sym;
+        }
+        __syncthreads();
+        flush_tile(tile, outb, n, N, blk, k0, rows, vec_ok);
+        __syncthreads();
+    }
+    if (!GENERIC && active && consumed > 8ull * L) err = true;
+    if (err) a.status[b] = ZR_INVALID_INPUT;
+}
+
+__global__ __launch_bounds__(64) void k_dec_x1(const uint8_t *enc, uint8_t *raw, KArgs a) {
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    if (n == 0 || !single_mode(n, a.N)) return;
+    const uint64_t len = a.enc_len[b];
+    if (len < 8) {  // "rANS data too short" (rans.rs:524-526)
+        a.status[b] = ZR_INVALID_INPUT;
+        return;
+    }
+    const RansDTab *T = tab_for(a.tables, a.table_stride, b);
+    const uint8_t *e = enc + a.enc_off[b];
+    uint64_t X = ld_u64_u(e + len - 8);
+    uint64_t pos = len - 8;
+    uint8_t *out = raw + a.raw_off[b];
+    for (uint64_t i = 0; i < n; i++) {
+        while (X < RANS_L) {
+            if (pos == 0) {
+                a.status[b] = ZR_INVALID_INPUT;
+                return;
+            }
+            pos--;
+            X = (X << 8) | e[pos];
+        }
+        const uint32_t slot = (uint32_t)(X & (TOTFREQ - 1));
+        const uint32_t sy = T->slot[slot] & 0xFF;
+        X = (uint64_t)T->freq[sy] * (X >> TF_SHIFT) + slot - T->start[sy];
+        out[i] = (uint8_t)sy;
+    }
+}
+
+// ======================================================================
+// host launchers
+// ======================================================================
+size_t rans_workspace_bytes(uint32_t B, uint32_t N, uint64_t max_len) {
+    if (N == 0) N = 1;
+    const uint64_t nblk = ceil_div(N, 256);
+    const uint64_t cmax = ceil_div(max_len ? max_len : 1, N);
+    const uint64_t cap = round_up(2 * cmax + 16, 16);
+    const uint64_t region = std::max<uint64_t>(round_up((uint64_t)N * cap, 256),
+                                               round_up(2 * max_len + 16, 256));
+    size_t t = 0;
+    t += round_up((uint64_t)B * N * 4, 256) * 2;
+    t += round_up((uint64_t)B * nblk * 8, 256) * 2;
+    t += round_up((uint64_t)B * nblk * 4, 256);
+    t += (size_t)B * region;
+    return t + 256;
+}
+
+int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t bytes, RansWork *w) {
+    if (N == 0) N = 1;
+    if (bytes < rans_workspace_bytes(B, N, max_len))
+        return set_error(ZR_INVALID_INPUT, "rANS workspace too small");
+    const uint64_t nblk = ceil_div(N, 256);
+    const uint64_t cmax = ceil_div(max_len ? max_len : 1, N);
+    w->cap = (uint32_t)round_up(2 * cmax + 16, 16);
+    w->region = std::max<uint64_t>(round_up((uint64_t)N * w->cap, 256), round_up(2 * max_len + 16, 256));
+    w->nblk = (uint32_t)nblk;
+    uint8_t *p = reinterpret_cast<uint8_t *>(round_up((uintptr_t)ws, 256));
+    auto take = [&](uint64_t n) {
+        uint8_t *r = p;
+        p += round_up(n, 256);
+        return r;
+    };
+    w->st_state = reinterpret_cast<uint32_t *>(take((uint64_t)B * N * 4));
+    w->st_len = reinterpret_cast<uint32_t *>(take((uint64_t)B * N * 4));
+    w->blocksum = reinterpret_cast<uint64_t *>(take((uint64_t)B * nblk * 8));
+    w->blockoff = reinterpret_cast<uint64_t *>(take((uint64_t)B * nblk * 8));
+    w->redo = reinterpret_cast<uint32_t *>(take((uint64_t)B * nblk * 4));
+    w->scratch = take((uint64_t)B * w->region);
+    return ZR_OK;
+}
+
+static KArgs kargs(const zr_rans_batch *bt) {
+    KArgs a;
+    a.B = bt->n_buffers;
+    a.N = bt->n_streams ? bt->n_streams : 1;
+    a.max_len = bt->max_len;
+    a.len = bt->len;
+    a.raw_off = bt->raw_off;
+    a.enc_off = bt->enc_off;
+    a.enc_len = bt->enc_len;
+    a.status = bt->status;
+    a.tables = bt->tables;
+    a.table_stride = bt->table_stride;
+    return a;
+}
+
+}  // namespace zr
+
+using namespace zr;
+
+extern "C" {
+
+size_t zr_rans_dtab_bytes(void) { return sizeof(RansDTab); }
+
+size_t zr_rans_workspace_bytes(uint32_t n_buffers, uint32_t n_streams, uint64_t max_len) {
+    return rans_workspace_bytes(n_buffers, n_streams, max_len);
+}
+
+int32_t zr_histogram_dev(const uint8_t *raw, const zr_rans_batch *bt, int32_t shared,
+                         uint32_t *hist_dev, void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!bt || !hist_dev) return set_error(ZR_INVALID_INPUT, "null argument");
+    if (bt->n_buffers == 0 || bt->max_len == 0) return ZR_OK;
+    KArgs a = kargs(bt);
+    const uint64_t chunk = 64 * 1024;
+    const uint32_t nchunk = (uint32_t)ceil_div(bt->max_len, chunk);
+    const uint64_t grid = (uint64_t)nchunk * a.B;
+    timer_begin("histogram", (hipStream_t)stream);
+    hipLaunchKernelGGL(k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a,
+                       shared, hist_dev, chunk, nchunk);
+    timer_end("histogram", (hipStream_t)stream);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_rans_dtab_from_hist_dev(const uint32_t *hist_dev, uint32_t n_tables, void *dtabs_dev,
+                                   void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (n_tables == 0) return ZR_OK;
+    hipLaunchKernelGGL(k_tab, dim3(n_tables), dim3(256), 0, (hipStream_t)stream, hist_dev,
+                       reinterpret_cast<RansDTab *>(dtabs_dev));
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, uint8_t *enc,
+                                 void *ws, size_t ws_bytes, void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!bt) return set_error(ZR_INVALID_INPUT, "null batch");
+    if (bt->n_buffers == 0) return ZR_OK;
+    KArgs a = kargs(bt);
+    RansWork w;
+    int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
+    if (st) return st;
+    hipStream_t s = (hipStream_t)stream;
+    ZR_HIP(hipMemsetAsync(bt->status, 0, sizeof(int32_t) * a.B, s));
+    const uint64_t gx = (uint64_t)w.nblk * a.B;
+    if (bt->max_len >= a.N && a.N > 1) {
+        timer_begin("rans_encode", s);
+        hipLaunchKernelGGL(k_enc_xn, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
+        timer_end("rans_encode", s);
+        hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
+        timer_begin("rans_compact", s);
+        hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
+        timer_end("rans_compact", s);
+    }
+    hipLaunchKernelGGL(k_enc_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, raw, a, w);
+    hipLaunchKernelGGL(k_enc_x1_compact, dim3(a.B), dim3(64), 0, s, enc, a, w);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, uint8_t *raw, void *ws,
+                                 size_t ws_bytes, void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!bt) return set_error(ZR_INVALID_INPUT, "null batch");
+    if (bt->n_buffers == 0) return ZR_OK;
+    KArgs a = kargs(bt);
+    RansWork w;
+    int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
+    if (st) return st;
+    hipStream_t s = (hipStream_t)stream;
+    ZR_HIP(hipMemsetAsync(bt->status, 0, sizeof(int32_t) * a.B, s));
+    const uint64_t gx = (uint64_t)w.nblk * a.B;
+    if (bt->max_len >= a.N && a.N > 1) {
+        hipLaunchKernelGGL(k_dec_hdr, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
+        hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
+        timer_begin("rans_decode", s);
+        hipLaunchKernelGGL(k_dec_xn<false>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
+        timer_end("rans_decode", s);
+        hipLaunchKernelGGL(k_dec_xn<true>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
+    }
+    hipLaunchKernelGGL(k_dec_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, enc, raw, a);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+"""Device-resident batch pipeline over the C ABI (torch supplies device memory and streams).
+
+A batch is B independent buffers, each one reference rANS stream set with
+P::N = n_streams. Buffers live contiguously in one raw area and one encoded
+area; offsets are device uint64 tensors. This is the hot path bench.py times.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from .errors import ZiporaError, check
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class RansDeviceBatch:
+    """Geometry + workspace for batched rANS on one GPU.
+
+    lens: list/tensor of decoded lengths; buffers are packed back to back in the
+    raw area (raw_off) and at fixed bound-sized slots in the encoded area
+    (enc_off), so encode needs no host round trip.
+    """
+
+    def __init__(self, lens, n_streams, device="cuda", shared_table=False, align=16):
+        self.L = _lib.load()
+        lens = [int(x) for x in lens]
+        self.B = len(lens)
+        self.N = int(n_streams)
+        self.device = torch.device(device)
+        self.max_len = max(lens) if lens else 0
+        raw_off, enc_off = [], []
+        r = e = 0
+        for n in lens:
+            raw_off.append(r)
+            enc_off.append(e)
+            r += (n + align - 1) // align * align
+            e += (self.L.zr_rans_encode_bound(n, self.N) + align - 1) // align * align
+        self.raw_bytes, self.enc_bytes = r, e
+        self.lens_host = lens
+        self.raw_off_host, self.enc_off_host = raw_off, enc_off
+        dev = self.device
+        u64 = torch.uint64 if hasattr(torch, "uint64") else torch.int64
+        self.len = torch.tensor(lens, dtype=torch.int64, device=dev)
+        self.raw_off = torch.tensor(raw_off, dtype=torch.int64, device=dev)
+        self.enc_off = torch.tensor(enc_off, dtype=torch.int64, device=dev)
+        self.enc_len = torch.zeros(self.B, dtype=torch.int64, device=dev)
+        self.status = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self.shared = bool(shared_table)
+        self.n_tables = 1 if self.shared else self.B
+        tb = self.L.zr_rans_dtab_bytes()
+        self.tables = torch.zeros(self.n_tables * tb, dtype=torch.uint8, device=dev)
+        self.hist = torch.zeros(self.n_tables * 256, dtype=torch.int32, device=dev)
+        wsb = self.L.zr_rans_workspace_bytes(self.B, self.N, self.max_len)
+        self.ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        self.ws_bytes = wsb
+        self.cbatch = _lib.RansBatch()
+        c = self.cbatch
+        c.n_buffers, c.n_streams, c.max_len = self.B, self.N, self.max_len
+        c.len, c.raw_off, c.enc_off = self.len.data_ptr(), self.raw_off.data_ptr(), self.enc_off.data_ptr()
+        c.enc_len, c.status = self.enc_len.data_ptr(), self.status.data_ptr()
+        c.tables = self.tables.data_ptr()
+        c.table_stride = 0 if self.shared else 1
+
+    # ---- areas
+    def new_raw(self):
+        return torch.zeros(max(1, self.raw_bytes), dtype=torch.uint8, device=self.device)
+
+    def new_enc(self):
+        return torch.zeros(max(1, self.enc_bytes), dtype=torch.uint8, device=self.device)
+
+    # ---- pipeline stages
+    def histogram(self, raw, stream=None):
+        check(self.L.zr_memset_dev(_ptr(self.hist), 0, self.hist.numel() * 4, _stream(stream)))
+        check(self.L.zr_histogram_dev(_ptr(raw), ctypes.byref(self.cbatch), int(self.shared),
+                                      _ptr(self.hist), _stream(stream)))
+
+    def tables_from_hist(self, stream=None):
+        check(self.L.zr_rans_dtab_from_hist_dev(_ptr(self.hist), self.n_tables, _ptr(self.tables),
+                                                _stream(stream)))
+
+    def upload_tables(self, host_tables):
+        arr = (_lib.RansTable * len(host_tables))(*host_tables)
+        check(self.L.zr_rans_dtab_upload(arr, len(host_tables), _ptr(self.tables), _stream()))
+
+    def encode(self, raw, enc, stream=None):
+        check(self.L.zr_rans_encode_batch_dev(ctypes.byref(self.cbatch), _ptr(raw), _ptr(enc),
+                                              _ptr(self.ws), self.ws_bytes, _stream(stream)))
+
+    def decode(self, enc, raw, stream=None):
+        check(self.L.zr_rans_decode_batch_dev(ctypes.byref(self.cbatch), _ptr(enc), _ptr(raw),
+                                              _ptr(self.ws), self.ws_bytes, _stream(stream)))
+
+    def full_encode(self, raw, enc, stream=None):
+        """histogram -> Rans64Encoder::new on device -> encode (no host round trip)."""
+        self.histogram(raw, stream)
+        self.tables_from_hist(stream)
+        self.encode(raw, enc, stream)
+
+    # ---- results
+    def statuses(self):
+        return self.status.cpu().tolist()
+
+    def raise_on_error(self):
+        st = self.statuses()
+        bad = [i for i, s in enumerate(st) if s != 0]
+        if bad:
+            raise ZiporaError(_lib.ZR_INVALID_INPUT, f"rANS batch: buffers {bad[:8]} failed")
+
+    def encoded(self, enc, b):
+        off = self.enc_off_host[b]
+        n = int(self.enc_len[b].item())
+        return bytes(enc[off: off + n].cpu().numpy().tobytes())
+
+    def raw_of(self, raw, b):
+        off = self.raw_off_host[b]
+        return bytes(raw[off: off + self.lens_host[b]].cpu().numpy().tobytes())

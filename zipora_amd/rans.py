@@ -1,0 +1,98 @@
+"""rANS order-0 -- host mirror of src/entropy/rans.rs over the HIP C ABI.
+
+Same names and argument meaning as the reference:
+  Rans64Encoder(frequencies, P).encode(data)           rans.rs:208, :338
+  Rans64Decoder(encoder).decode(encoded, output_length) rans.rs:449, :510
+P is the stream count of rans::ParallelVariant (rans.rs:165-196): the
+reference's ParallelX1/X2/X4/X8 plus any other N (the trait is public).
+Errors raise ZiporaError (InvalidData), like Result<_, ZiporaError>.
+"""
+import ctypes
+
+from . import _lib
+from .errors import ZiporaError, check
+
+
+class ParallelVariant:
+    def __init__(self, n, name=None):
+        self.N = int(n)
+        self.NAME = name or f"x{n}"
+
+
+ParallelX1 = ParallelVariant(1, "x1")
+ParallelX2 = ParallelVariant(2, "x2")
+ParallelX4 = ParallelVariant(4, "x4")
+ParallelX8 = ParallelVariant(8, "x8")
+
+
+def _variant(p):
+    return p if isinstance(p, ParallelVariant) else ParallelVariant(int(p))
+
+
+def _u8(data):
+    data = bytes(data)
+    return (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0"), len(data)
+
+
+class Rans64Symbol:
+    def __init__(self, start, freq):
+        self.start = start
+        self.freq = freq
+
+
+class Rans64Encoder:
+    """Rans64Encoder::<P>::new(&[u32; 256]) (rans.rs:208-235)."""
+
+    def __init__(self, frequencies, parallel=ParallelX1):
+        self.P = _variant(parallel)
+        freqs = [int(f) & 0xFFFFFFFF for f in frequencies]
+        if len(freqs) != 256:
+            raise ValueError("frequencies must have 256 entries")
+        self.table = _lib.RansTable()
+        arr = (ctypes.c_uint32 * 256)(*freqs)
+        check(_lib.load().zr_rans_table_build(arr, ctypes.byref(self.table)))
+
+    def encode(self, data):
+        """Rans64Encoder::encode (rans.rs:338-420)."""
+        L = _lib.load()
+        buf, n = _u8(data)
+        cap = L.zr_rans_encode_bound(n, self.P.N)
+        out = (ctypes.c_uint8 * cap)()
+        ol = ctypes.c_size_t(0)
+        check(L.zr_rans_encode(ctypes.byref(self.table), self.P.N, buf, n, out, cap, ctypes.byref(ol)))
+        return ctypes.string_at(out, ol.value)
+
+    def get_symbol(self, symbol):
+        return Rans64Symbol(self.table.start[symbol], self.table.freq[symbol])
+
+    def total_freq(self):
+        return self.table.total_freq
+
+    def variant_name(self):
+        return self.P.NAME
+
+
+class Rans64Decoder:
+    """Rans64Decoder::<P>::new(&encoder) (rans.rs:449-468)."""
+
+    def __init__(self, encoder):
+        self.P = encoder.P
+        self.table = encoder.table
+
+    def decode(self, encoded_data, output_length):
+        """Rans64Decoder::decode (rans.rs:510-651)."""
+        L = _lib.load()
+        buf, n = _u8(encoded_data)
+        out = (ctypes.c_uint8 * max(1, output_length))()
+        check(L.zr_rans_decode(ctypes.byref(self.table), self.P.N, buf, n, out, output_length))
+        return ctypes.string_at(out, output_length)
+
+
+def histogram(data):
+    import numpy as np
+    d = np.frombuffer(bytes(data), dtype=np.uint8)
+    return [int(x) for x in np.bincount(d, minlength=256)]
+
+
+__all__ = ["ParallelVariant", "ParallelX1", "ParallelX2", "ParallelX4", "ParallelX8",
+           "Rans64Encoder", "Rans64Decoder", "Rans64Symbol", "ZiporaError", "histogram"]
