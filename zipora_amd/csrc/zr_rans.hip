@@ -228,43 +228,101 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         et[v] = make_uint2(T->freq[v] | (T->start[v] << 13), T->rcp[v] | (T->rsh[v] << 27));
     }
     __syncthreads();
+    // Input rows k*N + 256*blk .. +255 are staged through an LDS tile of ETILE rows:
+    // each thread moves one 16-byte piece per tile (coalesced), loaded into
+    // registers one tile ahead (the loads fly while the previous tile is coded).
+    constexpr uint32_t ETILE = 16;
+    __shared__ __attribute__((aligned(16))) uint8_t itile[ETILE * 256];
     const uint32_t s = blk * 256 + threadIdx.x;
     const bool active = s < N;
     const uint64_t c = active ? (n - s - 1) / N + 1 : 0;  // symbols s, s+N, ... < n
     const uint64_t cmax = (n - 1) / N + 1;
-    const uint8_t *in = raw + a.raw_off[b] + s;
+    const uint8_t *inb = raw + a.raw_off[b];
+    const bool vec_in = ((((uintptr_t)inb) | N) & 15) == 0;
+    const uint32_t lr = threadIdx.x >> 4, lp = (threadIdx.x & 15) * 16;  // my piece: row, column
+    auto load_piece = [&](uint64_t t) -> uint4 {
+        const uint64_t k = t * ETILE + lr;
+        const uint64_t p = k * N + (uint64_t)blk * 256 + lp;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < cmax && blk * 256 + lp < N) {
+            if (vec_in && p + 16 <= n) {
+                v = *reinterpret_cast<const uint4 *>(inb + p);
+            } else {
+                uint32_t wv[4] = {0, 0, 0, 0};
+                for (uint32_t j = 0; j < 16; j++)
+                    if (p + j < n && blk * 256 + lp + j < N) wv[j >> 2] |= (uint32_t)inb[p + j] << (8 * (j & 3));
+                v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+            }
+        }
+        return v;
+    };
     uint32_t *out = reinterpret_cast<uint32_t *>(w.scratch + (size_t)b * w.region + (size_t)s * w.cap);
-    uint32_t x = RANS_L, acc = 0, nacc = 0, nout = 0;  // nout = dwords stored
+    uint32_t x = RANS_L, nout = 0;  // nout = dwords stored
+    uint64_t acc = 0;               // pending output bits (emission order from bit 0)
+    uint32_t nacc = 0;              // valid bits in acc, < 32 after every flush
     bool err = false;
-    for (uint64_t k = cmax; k-- > 0;) {
-        if (k < c && !err) {
-            const uint32_t sym = in[k * N];
-            const uint2 e = et[sym];
-            const uint32_t f = e.x & 0x1FFF;
-            if (f == 0) {  // "Symbol {} not in frequency table" (rans.rs:311-316)
-                err = true;
-                continue;
-            }
-            const uint32_t xmax = f << TF_SHIFT;  // ((L << 8) / TOTFREQ) * freq (rans.rs:319)
+    // encode_symbol (rans.rs:303-335), branchless: at most two renorm bytes
+    // (x < 2^24, xmax >= 2^12); q = x / f by the exact 24-bit reciprocal.
+    auto enc_step = [&](uint2 e, bool valid) {
+        const uint32_t f = e.x & 0x1FFF;
+        err |= valid && f == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
+        const uint32_t xmax = f << TF_SHIFT;  // ((L << 8) / TOTFREQ) * freq (rans.rs:319)
+        const bool c1 = valid && x >= xmax;
+        const uint32_t b1 = x & 0xFF;
+        uint32_t y = c1 ? x >> 8 : x;
+        const bool c2 = valid && y >= xmax;
+        const uint32_t b2 = y & 0xFF;
+        y = c2 ? y >> 8 : y;
+        const uint32_t nb = (c1 ? 8u : 0u) + (c2 ? 8u : 0u);
+        const uint32_t bytes = __builtin_amdgcn_ubfe(b1 | (b2 << 8), 0, nb);
+        acc |= (uint64_t)bytes << nacc;
+        nacc += nb;
+        const uint32_t q = __umulhi(y << 8, e.y & 0x7FFFFFF) >> (e.y >> 27);  // y / f
+        const uint32_t xn = y + (e.x >> 13) + q * (TOTFREQ - f);  // (y/f)*4096 + y%f + start
+        x = valid ? xn : x;
+    };
+    auto flush = [&]() {
+        if (nacc >= 32) {
+            out[nout++] = (uint32_t)acc;
+            acc >>= 32;
+            nacc -= 32;
+        }
+    };
+    const uint64_t ntiles = (cmax + ETILE - 1) / ETILE;
+    uint4 pend = load_piece(ntiles - 1);
+    for (uint64_t t = ntiles; t-- > 0;) {
+        __syncthreads();
+        *reinterpret_cast<uint4 *>(&itile[lr * 256 + lp]) = pend;
+        __syncthreads();
+        if (t > 0) pend = load_piece(t - 1);
+        const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
+        if (rtop == ETILE && t * ETILE + ETILE < cmax) {
+            // full tile: every row is complete for every stream (rows < cmax - 1)
 #pragma unroll
-            for (int r = 0; r < 2; r++) {  // x < 2^24 and xmax >= 2^12: at most 2 bytes
-                if (x >= xmax) {
-                    acc |= (x & 0xFF) << (8 * nacc);
-                    x >>= 8;
-                    if (++nacc == 4) {
-                        out[nout++] = acc;
-                        acc = 0;
-                        nacc = 0;
-                    }
-                }
+            for (int g = ETILE - 4; g >= 0; g -= 4) {
+                const uint32_t s3 = itile[(g + 3) * 256 + threadIdx.x], s2 = itile[(g + 2) * 256 + threadIdx.x];
+                const uint32_t s1 = itile[(g + 1) * 256 + threadIdx.x], s0 = itile[g * 256 + threadIdx.x];
+                const uint2 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
+                enc_step(e3, active);
+                enc_step(e2, active);
+                flush();
+                enc_step(e1, active);
+                enc_step(e0, active);
+                flush();
             }
-            const uint32_t q = __umulhi(x << 8, e.y & 0x7FFFFFF) >> (e.y >> 27);  // x / f
-            x = x + (e.x >> 13) + q * (TOTFREQ - f);  // (x/f)*4096 + x%f + start
+        } else {
+            for (uint32_t r = rtop; r-- > 0;) {
+                const uint64_t k = t * ETILE + r;
+                const uint32_t sym = itile[r * 256 + threadIdx.x];
+                enc_step(et[sym], k < c);
+                flush();
+            }
         }
     }
-    if (nacc) out[nout] = acc;
+    if (nacc) out[nout] = (uint32_t)acc;
+    const uint32_t nacc_bytes = nacc / 8;
     if (err) atomicOr(&a.status[b], 1);  // marked; converted to ZR_INVALID_INPUT by the scan
-    const uint32_t bytes = nout * 4 + nacc;
+    const uint32_t bytes = nout * 4 + nacc_bytes;
     if (active) {
         w.st_state[(size_t)b * N + s] = x;
         w.st_len[(size_t)b * N + s] = bytes;
@@ -362,7 +420,9 @@ __global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, Rans
         st_u32_u(e + 8 * (size_t)N + 4 * (size_t)s, L);
     }
     __syncthreads();
-    // each wave copies 64 streams, all lanes on one stream at a time
+    // each wave copies 64 streams, all lanes on one stream at a time: lane i
+    // writes the i-th 16-byte ALIGNED chunk of the destination range; interior
+    // chunks gather their 16 source bytes with 5 dword loads + v_alignbyte.
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint8_t *dbase = e + 12 * (size_t)N;
     for (int j = wv * 64; j < wv * 64 + 64; j++) {
@@ -370,8 +430,29 @@ __global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, Rans
         if (sj >= N) break;
         const uint8_t *src = w.scratch + (size_t)b * w.region + (size_t)sj * w.cap;
         uint8_t *dst = dbase + soff[j];
-        const uint32_t Lj = slen[j];
-        for (uint32_t i = lane; i < Lj; i += 64) dst[i] = src[i];
+        const int64_t Lj = slen[j];
+        if (Lj == 0) continue;
+        const uintptr_t da0 = (uintptr_t)dst & ~(uintptr_t)15;
+        const uint64_t nch = ((uintptr_t)dst + Lj - da0 + 15) / 16;
+        for (uint64_t cidx = lane; cidx < nch; cidx += 64) {
+            const uintptr_t da = da0 + 16 * cidx;
+            const int64_t o = (int64_t)(da - (uintptr_t)dst);  // source offset of the chunk
+            if (o >= 0 && o + 16 <= Lj) {
+                const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src + (o & ~(int64_t)3));
+                const uint32_t r = (uint32_t)(o & 3) * 8;
+                const uint32_t w0 = s4[0], w1 = s4[1], w2 = s4[2], w3 = s4[3], w4 = s4[4];
+                uint4 v;
+                v.x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> r);
+                v.y = (uint32_t)((((uint64_t)w2 << 32) | w1) >> r);
+                v.z = (uint32_t)((((uint64_t)w3 << 32) | w2) >> r);
+                v.w = (uint32_t)((((uint64_t)w4 << 32) | w3) >> r);
+                *reinterpret_cast<uint4 *>(da) = v;
+            } else {
+                const int64_t lo_b = o < 0 ? -o : 0;
+                const int64_t hi_b = o + 16 <= Lj ? 16 : Lj - o;
+                for (int64_t t = lo_b; t < hi_b; t++) reinterpret_cast<uint8_t *>(da)[t] = src[o + t];
+            }
+        }
     }
 }
 
@@ -565,6 +646,228 @@ __global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw
     if (err) a.status[b] = ZR_INVALID_INPUT;
 }
 
+// ----------------------------------------------------------------------
+// Fast xN decode. One lane = one stream, FW = 512 lanes per workgroup share
+// one 16 KiB LDS slot table (2 workgroups per CU hold 1024 streams).
+//   * stream bytes: per-lane ring of RSLOTS x 16 B in LDS, layout [slot][lane].
+//     Ring refills are wave-UNIFORM: every DTILE steps each lane writes the
+//     chunks it loaded DTILE steps earlier (register staged, so the global
+//     load latency overlaps a whole tile) and issues loads for up to two more.
+//     A lane only ever reads its own ring column, so no barrier is needed.
+//   * window: 64-bit MSB-first bit window refilled by one aligned dword per
+//     refill; the next dword is prefetched from the ring with the table read.
+//   * output: 4 steps per lane are packed into a dword and 4x4-byte
+//     transposed across each lane quad with DPP, so every lane stores one
+//     aligned dword per 4 steps: row k+q, streams s0..s0+3.
+// ----------------------------------------------------------------------
+constexpr int FW = 512;
+constexpr int RSLOTS = 8;
+constexpr int DTILE = 16;
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void asm_load16(v4u &dst, uintptr_t addr) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(addr) : "memory");
+}
+
+__device__ __forceinline__ uint32_t dpp_xor2(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+}
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+}
+
+__global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
+                                                 uint32_t nblkF) {
+    const uint32_t b = blockIdx.x / nblkF, blkF = blockIdx.x % nblkF;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    const uint32_t N = a.N;
+    if (n == 0 || single_mode(n, N) || a.status[b] != 0) return;
+    constexpr uint32_t RB = RSLOTS * 16;  // ring bytes per lane
+    __shared__ uint32_t stab[TOTFREQ];
+    __shared__ __attribute__((aligned(16))) uint8_t ringb[FW * RB];  // [lane][RB], chunk slots swizzled
+    // scan scratch and flag alias the ring (used before it is filled): keeps the
+    // workgroup at exactly 80 KiB of LDS so two fit on a CU
+    unsigned long long *sh = reinterpret_cast<unsigned long long *>(ringb);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(ringb) + 64;
+    const uint32_t tid = threadIdx.x;
+    const RansDTab *T = tab_for(a.tables, a.table_stride, b);
+    for (uint32_t j = tid; j < TOTFREQ; j += FW) stab[j] = T->slot[j];
+    const uint32_t kind = T->kind;
+    const uint32_t s = blkF * FW + tid;
+    const bool active = s < N;
+    const uint8_t *e = enc + a.enc_off[b];
+    const uint32_t L = active ? ld_u32_u(e + 8 * (size_t)N + 4 * (size_t)s) : 0;
+    // 512-lane exclusive scan of the stream lengths + base of the first 256-block
+    unsigned long long inc = wave_incl_scan(L);
+    const int wv = tid >> 6;
+    if ((tid & 63) == 63) sh[wv] = inc;
+    if (tid == 0) *flag = 0;
+    __syncthreads();
+    unsigned long long base = 0;
+    for (int i = 0; i < wv; i++) base += sh[i];
+    const uint64_t off = base + inc - L + w.blockoff[(size_t)b * w.nblk + 2 * blkF];
+    const uint64_t X = active ? ld_u64_u(e + 8 * (size_t)s) : RANS_L;
+    uint8_t *outb = raw + a.raw_off[b];
+    const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24) && (N & 3) == 0 &&
+                      (((uintptr_t)outb) & 3) == 0;
+    if (!fast) atomicOr(flag, 1u);
+    __syncthreads();
+    const uint32_t any_slow = *flag;
+    __syncthreads();  // scan/flag reads complete before the ring is written
+    if (any_slow) {
+        if (tid == 0) {
+            w.redo[(size_t)b * w.nblk + 2 * blkF] = 1;
+            if (2 * blkF + 1 < w.nblk) w.redo[(size_t)b * w.nblk + 2 * blkF + 1] = 1;
+        }
+        return;
+    }
+    const uint64_t c = active ? (n - s - 1) / N + 1 : 0;
+    const uint64_t cmax = (n - 1) / N + 1;
+    const uintptr_t sb = (uintptr_t)e + 12 * (size_t)N + off;  // stream start
+    const uintptr_t lo_lim = ((uintptr_t)e) & ~(uintptr_t)15;     // safe lower bound for loads
+    const uint32_t lanebase = tid * RB;
+    const uint32_t lanex = (tid & (RSLOTS - 1)) << 4;  // slot swizzle: spreads equal offsets over banks
+    auto roff = [&](uint32_t addr) -> uint32_t { return lanebase + ((addr & (RB - 1)) ^ lanex); };
+    auto lds32 = [&](uint32_t o) -> uint32_t { return *reinterpret_cast<const uint32_t *>(ringb + o); };
+    auto clampa = [&](uintptr_t addr) -> uintptr_t { return addr > lo_lim ? addr : lo_lim; };
+    // ---- ring prologue: the 4 chunks ending at the stream end, synchronously
+    const uintptr_t pend = sb + L;
+    uintptr_t lo = ((pend - 1) & ~(uintptr_t)15) + 16;  // lowest chunk loaded or in flight
+    {
+        const v4u c0 = *reinterpret_cast<const v4u *>(clampa(lo - 16));
+        const v4u c1 = *reinterpret_cast<const v4u *>(clampa(lo - 32));
+        const v4u c2 = *reinterpret_cast<const v4u *>(clampa(lo - 48));
+        const v4u c3 = *reinterpret_cast<const v4u *>(clampa(lo - 64));
+        *reinterpret_cast<v4u *>(ringb + roff((uint32_t)(lo - 16))) = c0;
+        *reinterpret_cast<v4u *>(ringb + roff((uint32_t)(lo - 32))) = c1;
+        *reinterpret_cast<v4u *>(ringb + roff((uint32_t)(lo - 48))) = c2;
+        *reinterpret_cast<v4u *>(ringb + roff((uint32_t)(lo - 64))) = c3;
+        lo -= 64;
+    }
+    // window: the dword holding the last stream byte, its garbage top bytes shifted out
+    const uintptr_t a0 = (pend - 1) & ~(uintptr_t)3;
+    const uint32_t v0 = (uint32_t)(pend - a0);
+    uint32_t x = (uint32_t)X;
+    uint64_t win = (uint64_t)(lds32(roff((uint32_t)a0)) << (32 - 8 * v0)) << 32;
+    uint32_t nbits = 8 * v0;
+    const uint32_t pend32 = (uint32_t)pend;
+    uint32_t cons = (uint32_t)a0;  // (low 32 bits) bytes [cons, pend) have entered the window
+    uint32_t nextw = lds32(roff(cons - 4));
+    // staged chunks in flight. Inline asm so hipcc inserts no conservative
+    // vmcnt(0) (it would also wait for the tile's stores); the boundary below
+    // waits with an exact count instead.
+    v4u st0, st1;
+    asm_load16(st0, clampa(lo - 16));
+    asm_load16(st1, clampa(lo - 32));
+    uint32_t nst = 2;
+    uint32_t stlo = (uint32_t)(lo - 32);
+    lo -= 32;
+    // quad transpose selectors
+    const uint32_t q = tid & 3;
+    const uint32_t sel1 = q < 2 ? 0x05040100u : 0x03020706u;
+    const uint32_t sel2 = (q & 1) ? 0x03070105u : 0x06020400u;
+    const uint64_t s0 = s & ~3u;
+    uint32_t cons_snap = cons;
+    uint32_t nbits_snap = nbits;
+    const bool wave_live = (uint64_t)blkF * FW + (tid & ~63u) < N;  // wave-uniform
+
+    // one decode step: renormalise (rans.rs:479-485) then decode (rans.rs:488-504)
+    auto step = [&](const uint32_t selj, uint32_t &wd) {
+        // x in [16, 2^24) needs 0, 1 or 2 bytes; the shift is 8 * #bytes
+        const uint32_t sh8 = (__builtin_clz(x) & 24) - 8;
+        x = (uint32_t)(((((uint64_t)x) << 32) | (uint32_t)(win >> 32)) << sh8 >> 32);
+        win <<= sh8;
+        nbits -= sh8;
+        // branchless refill of one dword from the ring
+        const bool need = nbits <= 32;
+        win |= (uint64_t)(need ? nextw : 0u) << ((32 - nbits) & 63);
+        nbits += need ? 32u : 0u;
+        cons -= need ? 4u : 0u;
+        nextw = lds32(roff(cons - 4));
+        const uint32_t ent = stab[x & (TOTFREQ - 1)];
+        x = __umul24(ent >> 20, x >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
+        wd = __builtin_amdgcn_perm(ent, wd, selj);
+    };
+    // 4x4 byte transpose across the lane quad: lane q gets row kg+q of streams s0..s0+3
+    auto quad_t = [&](uint32_t wd) -> uint32_t {
+        const uint32_t t1 = __builtin_amdgcn_perm(dpp_xor2(wd), wd, sel1);
+        return __builtin_amdgcn_perm(dpp_xor1(t1), t1, sel2);
+    };
+    constexpr uint32_t SEL0 = 0x03020104u, SEL1 = 0x03020400u, SEL2 = 0x03040100u, SEL3 = 0x04020100u;
+
+    bool prev_full = true;
+    for (uint64_t k0 = 0; k0 < cmax; k0 += DTILE) {
+        // ---- ring maintenance (wave-uniform position, per-lane masks)
+        if (k0 > 0) {
+            // the previous boundary's chunk loads are followed by exactly 4 dword
+            // stores of this wave when that tile was full and the wave is live
+            if (prev_full && wave_live) asm volatile("s_waitcnt vmcnt(4)" : "+v"(st0), "+v"(st1)::"memory");
+            else asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1)::"memory");
+            if (nst >= 1) *reinterpret_cast<v4u *>(ringb + roff(stlo + 16 * (nst - 1))) = st0;
+            if (nst >= 2) *reinterpret_cast<v4u *>(ringb + roff(stlo)) = st1;
+            const uint32_t lo32 = (uint32_t)lo;
+            const uint32_t occ = ((cons - 1 - lo32) >> 4) + 1;
+            const uint32_t nl = min(2u, RSLOTS > occ ? RSLOTS - occ : 0u);
+            nst = nl;
+            if (nl >= 1) asm_load16(st0, clampa(lo - 16));
+            if (nl >= 2) asm_load16(st1, clampa(lo - 32));
+            lo -= 16 * nl;
+            stlo = (uint32_t)lo;
+        }
+        const bool full = k0 + DTILE < cmax;  // every row of the tile is complete for every stream
+        if (full) {
+            uint8_t *rowp = outb + (k0 + q) * N + s0;
+#pragma unroll
+            for (int g = 0; g < DTILE / 4; g++) {
+                uint32_t wd = 0;
+                step(SEL0, wd);
+                step(SEL1, wd);
+                step(SEL2, wd);
+                step(SEL3, wd);
+                const uint32_t t2 = quad_t(wd);
+                if (s0 < N) *reinterpret_cast<uint32_t *>(rowp) = t2;
+                rowp += 4 * (uint64_t)N;
+            }
+        } else {
+            const uint32_t nsteps = (uint32_t)(cmax - k0);
+            for (uint32_t g = 0; g * 4 < nsteps; g++) {
+                const uint64_t kg = k0 + 4 * g;
+                uint32_t wd = 0;
+                const uint32_t sels[4] = {SEL0, SEL1, SEL2, SEL3};
+                for (int j = 0; j < 4; j++) {
+                    if (kg + j == c) {  // first step past this lane's symbols
+                        cons_snap = cons;
+                        nbits_snap = nbits;
+                    }
+                    step(sels[j], wd);
+                }
+                const uint32_t t2 = quad_t(wd);
+                const uint64_t pos = (kg + q) * N + s0;
+                if (s0 < N) {
+                    if (pos + 4 <= n) {
+                        *reinterpret_cast<uint32_t *>(outb + pos) = t2;
+                    } else {
+                        for (uint32_t j = 0; j < 4; j++)
+                            if (pos + j < n) outb[pos + j] = (uint8_t)(t2 >> (8 * j));
+                    }
+                }
+            }
+        }
+        prev_full = full;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1)::"memory");
+    if (c == cmax && cmax % 4 == 0) {  // no step past the end was executed for this lane
+        cons_snap = cons;
+        nbits_snap = nbits;
+    }
+    // bytes consumed by renormalisation = bytes moved into the window - bits still there
+    if (active) {
+        const uint64_t consumed = (uint64_t)(pend32 - cons_snap) - nbits_snap / 8;
+        if (consumed > L) a.status[b] = ZR_INVALID_INPUT;  // "Insufficient data" (rans.rs:480-482)
+    }
+}
+
 __global__ __launch_bounds__(64) void k_dec_x1(const uint8_t *enc, uint8_t *raw, KArgs a) {
     const uint32_t b = blockIdx.x * 64 + threadIdx.x;
     if (b >= a.B) return;
@@ -742,7 +1045,8 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
         hipLaunchKernelGGL(k_dec_hdr, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
         hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
         timer_begin("rans_decode", s);
-        hipLaunchKernelGGL(k_dec_xn<false>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
+        const uint32_t nblkF = (uint32_t)ceil_div(a.N, FW);
+        hipLaunchKernelGGL(k_dec_fast, dim3(nblkF * a.B), dim3(FW), 0, s, enc, raw, a, w, nblkF);
         timer_end("rans_decode", s);
         hipLaunchKernelGGL(k_dec_xn<true>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
     }
