@@ -12,6 +12,8 @@
 // is staged through an LDS tile and moved with 16-byte coalesced accesses.
 // The decode slot table (16 KiB) and encode symbol table (2 KiB) live in LDS.
 // Per-buffer x1 streams (blob records) run one lane per buffer.
+#include <cstdlib>
+
 #include "zr_internal.h"
 
 namespace zr {
@@ -210,22 +212,41 @@ __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tab
     }
 }
 
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void asm_load16(v4u &dst, uintptr_t addr) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(addr) : "memory");
+}
+
+// s_waitcnt vmcnt(min(n, 12)) with a runtime, wave-uniform n
+#define ZR_WAITC(k) \
+    case k:         \
+        asm volatile("s_waitcnt vmcnt(" #k ")" : "+v"(reg)::"memory"); \
+        break;
+__device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
+    switch (n > 12 ? 12 : n) {
+        ZR_WAITC(0) ZR_WAITC(1) ZR_WAITC(2) ZR_WAITC(3) ZR_WAITC(4) ZR_WAITC(5) ZR_WAITC(6)
+        ZR_WAITC(7) ZR_WAITC(8) ZR_WAITC(9) ZR_WAITC(10) ZR_WAITC(11) ZR_WAITC(12)
+    }
+}
+
 // ======================================================================
 // encode, xN layout: one lane per stream (rans.rs:369-420, encode_symbol :303-335)
 // ======================================================================
-__global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
+__global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w, int ablate) {
     const uint32_t nblk = w.nblk;
     const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
     if (single_mode(n, N)) return;
-    __shared__ uint2 et[256];  // x: freq | start << 13 ; y: rcp | rsh << 27
+    // per symbol: x = xmax = freq << 12 (0 = not in table), y = start,
+    // z = reciprocal, w = (4096 - freq) | rsh << 16
+    __shared__ uint4 et[256];
     __shared__ unsigned long long sh[4];
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
     {
-        const uint32_t v = threadIdx.x;
-        et[v] = make_uint2(T->freq[v] | (T->start[v] << 13), T->rcp[v] | (T->rsh[v] << 27));
+        const uint32_t v = threadIdx.x, f = T->freq[v];
+        et[v] = make_uint4(f << TF_SHIFT, T->start[v], T->rcp[v], (TOTFREQ - f) | (T->rsh[v] << 16));
     }
     __syncthreads();
     // Input rows k*N + 256*blk .. +255 are staged through an LDS tile of ETILE rows:
@@ -263,10 +284,9 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     bool err = false;
     // encode_symbol (rans.rs:303-335), branchless: at most two renorm bytes
     // (x < 2^24, xmax >= 2^12); q = x / f by the exact 24-bit reciprocal.
-    auto enc_step = [&](uint2 e, bool valid) {
-        const uint32_t f = e.x & 0x1FFF;
-        err |= valid && f == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
-        const uint32_t xmax = f << TF_SHIFT;  // ((L << 8) / TOTFREQ) * freq (rans.rs:319)
+    auto enc_step = [&](const uint4 e, bool valid) {
+        const uint32_t xmax = e.x;  // ((L << 8) / TOTFREQ) * freq (rans.rs:319)
+        err |= valid && xmax == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
         const bool c1 = valid && x >= xmax;
         const uint32_t b1 = x & 0xFF;
         uint32_t y = c1 ? x >> 8 : x;
@@ -277,24 +297,58 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         const uint32_t bytes = __builtin_amdgcn_ubfe(b1 | (b2 << 8), 0, nb);
         acc |= (uint64_t)bytes << nacc;
         nacc += nb;
-        const uint32_t q = __umulhi(y << 8, e.y & 0x7FFFFFF) >> (e.y >> 27);  // y / f
-        const uint32_t xn = y + (e.x >> 13) + q * (TOTFREQ - f);  // (y/f)*4096 + y%f + start
+        const uint32_t q = __umulhi(y << 8, e.z) >> (e.w >> 16);  // y / f
+        const uint32_t xn = y + e.y + __umul24(q, e.w & 0xFFFF);  // (y/f)*4096 + y%f + start
         x = valid ? xn : x;
     };
+    uint32_t sc = 0;  // store instructions this wave issued since the last piece load
+    // full dwords queue in a 4-dword shift register; a lane stores 16 bytes at
+    // once (dwordx4), so each wave store instruction touches few lane addresses
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0;
+    v4u *out4 = reinterpret_cast<v4u *>(out);
     auto flush = [&]() {
         if (nacc >= 32) {
-            out[nout++] = (uint32_t)acc;
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            q3 = (uint32_t)acc;
             acc >>= 32;
             nacc -= 32;
+            nq++;
+        }
+        const bool need = nq == 4;
+        if (__builtin_amdgcn_ballot_w64(need) != 0) {  // wave-uniform
+            sc++;
+            if (need) {
+                if (ablate & 1) asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3));  // diagnostic
+                else out4[nout >> 2] = v4u{q0, q1, q2, q3};
+                nout += 4;
+                nq = 0;
+            }
+        }
+    };
+    // piece prefetch: inline-asm loads (no compiler vmcnt(0) that would also
+    // wait for the scratch stores); the wait counts this wave's stores since.
+    auto issue_piece = [&](uint64_t t, v4u &dst) {
+        const uint64_t k = t * ETILE + lr;
+        const uint64_t p = k * N + (uint64_t)blk * 256 + lp;
+        if (vec_in && k < cmax && blk * 256 + lp + 16 <= N && p + 16 <= n) {
+            asm_load16(dst, (uintptr_t)(inb + p));
+        } else {
+            const uint4 v = load_piece(t);
+            dst = v4u{v.x, v.y, v.z, v.w};
         }
     };
     const uint64_t ntiles = (cmax + ETILE - 1) / ETILE;
-    uint4 pend = load_piece(ntiles - 1);
+    v4u pend;
+    issue_piece(ntiles - 1, pend);
     for (uint64_t t = ntiles; t-- > 0;) {
         __syncthreads();
-        *reinterpret_cast<uint4 *>(&itile[lr * 256 + lp]) = pend;
+        wait_vmcnt_le(sc, pend);
+        *reinterpret_cast<v4u *>(&itile[lr * 256 + lp]) = pend;
         __syncthreads();
-        if (t > 0) pend = load_piece(t - 1);
+        sc = 0;
+        if (t > 0) issue_piece(t - 1, pend);
         const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
         if (rtop == ETILE && t * ETILE + ETILE < cmax) {
             // full tile: every row is complete for every stream (rows < cmax - 1)
@@ -302,7 +356,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
             for (int g = ETILE - 4; g >= 0; g -= 4) {
                 const uint32_t s3 = itile[(g + 3) * 256 + threadIdx.x], s2 = itile[(g + 2) * 256 + threadIdx.x];
                 const uint32_t s1 = itile[(g + 1) * 256 + threadIdx.x], s0 = itile[g * 256 + threadIdx.x];
-                const uint2 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
+                const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
                 enc_step(e3, active);
                 enc_step(e2, active);
                 flush();
@@ -318,6 +372,13 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
                 flush();
             }
         }
+    }
+    wait_vmcnt_le(0, pend);
+    // drain: queued dwords (oldest in q[4-nq]) then the partial dword
+    {
+        const uint32_t qs[4] = {q0, q1, q2, q3};
+        for (uint32_t i = 0; i < nq; i++) out[nout + i] = qs[4 - nq + i];
+        nout += nq;
     }
     if (nacc) out[nout] = (uint32_t)acc;
     const uint32_t nacc_bytes = nacc / 8;
@@ -396,9 +457,11 @@ __global__ __launch_bounds__(256) void k_scan(KArgs a, RansWork w, int decode) {
 }
 
 // header + stream compaction of the xN layout (rans.rs:402-419)
+constexpr uint32_t CSPLIT = 4;  // workgroups per 256-stream block (more bytes in flight per CU)
 __global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, RansWork w) {
     const uint32_t nblk = w.nblk;
-    const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+    const uint32_t part = blockIdx.x % CSPLIT;
+    const uint32_t b = blockIdx.x / CSPLIT / nblk, blk = (blockIdx.x / CSPLIT) % nblk;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
@@ -413,31 +476,41 @@ __global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, Rans
     soff[threadIdx.x] = off;
     slen[threadIdx.x] = L;
     uint8_t *e = enc + a.enc_off[b];
-    if (active) {
+    if (active && part == 0) {
         const uint32_t x = w.st_state[(size_t)b * N + s];
         st_u32_u(e + 8 * (size_t)s, x);
         st_u32_u(e + 8 * (size_t)s + 4, 0);
         st_u32_u(e + 8 * (size_t)N + 4 * (size_t)s, L);
     }
     __syncthreads();
-    // each wave copies 64 streams, all lanes on one stream at a time: lane i
-    // writes the i-th 16-byte ALIGNED chunk of the destination range; interior
-    // chunks gather their 16 source bytes with 5 dword loads + v_alignbyte.
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // The block's 256 streams are contiguous in the destination. Each thread
+    // owns aligned 16-byte destination units (unit u = thread + 256 i) and
+    // finds the stream holding it by a forward scan of the stream offsets in
+    // LDS; interior units gather 16 source bytes with 5 dword loads +
+    // v_alignbyte, units crossing a stream boundary go byte by byte.
+    __shared__ uint64_t send_s[256];
+    send_s[threadIdx.x] = off + L;  // (exclusive end offsets, relative to the buffer's stream area)
+    __syncthreads();
     uint8_t *dbase = e + 12 * (size_t)N;
-    for (int j = wv * 64; j < wv * 64 + 64; j++) {
-        const uint32_t sj = blk * 256 + j;
-        if (sj >= N) break;
-        const uint8_t *src = w.scratch + (size_t)b * w.region + (size_t)sj * w.cap;
-        uint8_t *dst = dbase + soff[j];
-        const int64_t Lj = slen[j];
-        if (Lj == 0) continue;
-        const uintptr_t da0 = (uintptr_t)dst & ~(uintptr_t)15;
-        const uint64_t nch = ((uintptr_t)dst + Lj - da0 + 15) / 16;
-        for (uint64_t cidx = lane; cidx < nch; cidx += 64) {
-            const uintptr_t da = da0 + 16 * cidx;
-            const int64_t o = (int64_t)(da - (uintptr_t)dst);  // source offset of the chunk
-            if (o >= 0 && o + 16 <= Lj) {
+    const uint32_t nstream = min(256u, N - blk * 256);
+    const uint64_t r0 = soff[0], r1 = send_s[nstream - 1];  // destination range [r0, r1)
+    if (r1 > r0) {
+        const uintptr_t ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
+        const uint64_t nunits = ((uintptr_t)dbase + r1 - ua0 + 15) / 16;
+        const uint64_t ulo = nunits * part / CSPLIT, uhi = nunits * (part + 1) / CSPLIT;
+        uint32_t sj = 0;
+        for (uint64_t u = ulo + threadIdx.x; u < uhi; u += 256) {
+            const uintptr_t ua = ua0 + 16 * u;
+            // destination offset of the unit; negative for a first unit that starts in the header
+            const int64_t p0 = (int64_t)(ua - (uintptr_t)dbase);
+            while (sj + 1 < nstream && (int64_t)send_s[sj] <= p0) sj++;
+            const int64_t o = p0 - (int64_t)soff[sj];  // source offset in stream sj
+            const uint8_t *src = w.scratch + (size_t)b * w.region + (size_t)(blk * 256 + sj) * w.cap;
+            const uint8_t *sbase = w.scratch + (size_t)b * w.region + (size_t)(blk * 256) * w.cap;
+            // 16 source bytes of stream j starting at source offset o (o may be
+            // negative: bytes before the stream are read but masked off later)
+            auto gather16 = [&](uint32_t j, int64_t o) -> uint4 {
+                const uint8_t *src = sbase + (size_t)j * w.cap;
                 const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src + (o & ~(int64_t)3));
                 const uint32_t r = (uint32_t)(o & 3) * 8;
                 const uint32_t w0 = s4[0], w1 = s4[1], w2 = s4[2], w3 = s4[3], w4 = s4[4];
@@ -446,11 +519,35 @@ __global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, Rans
                 v.y = (uint32_t)((((uint64_t)w2 << 32) | w1) >> r);
                 v.z = (uint32_t)((((uint64_t)w3 << 32) | w2) >> r);
                 v.w = (uint32_t)((((uint64_t)w4 << 32) | w3) >> r);
-                *reinterpret_cast<uint4 *>(da) = v;
+                return v;
+            };
+            const int64_t endj = (int64_t)send_s[sj] - p0;  // unit bytes [0, endj) lie in stream sj
+            const bool inside = p0 >= (int64_t)r0 && p0 + 16 <= (int64_t)r1;
+            if (o >= 0 && endj >= 16) {
+                *reinterpret_cast<uint4 *>(ua) = gather16(sj, o);  // interior unit
+            } else if (inside && o >= 0 && sj + 1 < nstream &&
+                       ((int64_t)send_s[sj + 1] - p0 >= 16 || sj + 2 == nstream)) {
+                // unit crossing one stream boundary at byte endj: merge two gathers
+                const uint4 A = gather16(sj, o), Bv = gather16(sj + 1, -endj);
+                auto msk = [&](int i) -> uint32_t {
+                    const int64_t k = endj - 4 * i;  // bytes of dword i taken from A
+                    return k >= 4 ? 0xFFFFFFFFu : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
+                };
+                uint4 v;
+                v.x = (A.x & msk(0)) | (Bv.x & ~msk(0));
+                v.y = (A.y & msk(1)) | (Bv.y & ~msk(1));
+                v.z = (A.z & msk(2)) | (Bv.z & ~msk(2));
+                v.w = (A.w & msk(3)) | (Bv.w & ~msk(3));
+                *reinterpret_cast<uint4 *>(ua) = v;
             } else {
-                const int64_t lo_b = o < 0 ? -o : 0;
-                const int64_t hi_b = o + 16 <= Lj ? 16 : Lj - o;
-                for (int64_t t = lo_b; t < hi_b; t++) reinterpret_cast<uint8_t *>(da)[t] = src[o + t];
+                // range edge or a unit spanning three or more streams: byte by byte
+                uint32_t sk = sj;
+                for (int t = 0; t < 16; t++) {
+                    const int64_t p = p0 + t;
+                    if (p < (int64_t)r0 || p >= (int64_t)r1) continue;
+                    while (sk + 1 < nstream && (int64_t)send_s[sk] <= p) sk++;
+                    reinterpret_cast<uint8_t *>(ua)[t] = sbase[(size_t)sk * w.cap + (p - (int64_t)soff[sk])];
+                }
             }
         }
     }
@@ -663,11 +760,6 @@ __global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw
 constexpr int FW = 512;
 constexpr int RSLOTS = 8;
 constexpr int DTILE = 16;
-
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void asm_load16(v4u &dst, uintptr_t addr) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(addr) : "memory");
-}
 
 __device__ __forceinline__ uint32_t dpp_xor2(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
@@ -1014,11 +1106,12 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
     const uint64_t gx = (uint64_t)w.nblk * a.B;
     if (bt->max_len >= a.N && a.N > 1) {
         timer_begin("rans_encode", s);
-        hipLaunchKernelGGL(k_enc_xn, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
+        static const int ablate = getenv("ZR_ABLATE") ? atoi(getenv("ZR_ABLATE")) : 0;  // diagnostics only
+        hipLaunchKernelGGL(k_enc_xn, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w, ablate);
         timer_end("rans_encode", s);
         hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
         timer_begin("rans_compact", s);
-        hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
+        hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
         timer_end("rans_compact", s);
     }
     hipLaunchKernelGGL(k_enc_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, raw, a, w);
