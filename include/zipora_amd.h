@@ -108,6 +108,51 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *batch, const uint8_t *raw,
 int32_t zr_rans_decode_batch_dev(const zr_rans_batch *batch, const uint8_t *enc, uint8_t *raw,
                                  void *workspace, size_t workspace_bytes, void *stream);
 
+/* ======================================================================
+ * FSE (rANS with 32-bit renormalisation words) -- src/entropy/fse.rs
+ * Stream formats (Appendix A): 0xF5 single | 0xF6 nblocks sizes bodies.
+ * ====================================================================== */
+typedef struct {
+    uint32_t table_log;        /* FseConfig::table_log, validated 5..15 (coding uses 12, fse.rs:424-426) */
+    int32_t compression_level; /* 1..22 */
+    uint64_t max_table_size;
+    uint64_t parallel_blocks;  /* 0 = None, k = Some(k) */
+    uint64_t block_size;
+    int32_t adaptive;
+} zr_fse_config;               /* FseConfig, fse.rs:204-263 */
+
+void zr_fse_config_default(zr_fse_config *c);                     /* FseConfig::default */
+size_t zr_fse_compress_bound(size_t n, const zr_fse_config *c);
+/* FseEncoder::new(config)?.compress(data)              fse.rs:773, :854-884 */
+int32_t zr_fse_compress(const zr_fse_config *c, const uint8_t *in, size_t n, uint8_t *out,
+                        size_t out_cap, size_t *out_len);
+/* FseDecoder::new().decompress(data)                    fse.rs:1084, :1105-1312 */
+int32_t zr_fse_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                          size_t *out_len);
+/* FseEncoder::compress with a caller-given raw frequency table: the static
+ * table kept when adaptive=false (fse.rs:860-862) and with_dictionary's added
+ * dictionary counts (fse.rs:807-812). freqs == NULL: histogram of in. */
+int32_t zr_fse_compress_freqs(const zr_fse_config *c, const uint32_t *freqs, const uint8_t *in,
+                              size_t n, uint8_t *out, size_t out_cap, size_t *out_len);
+/* analyze_frequencies' byte histogram (fse.rs:796-851) on the device */
+int32_t zr_byte_histogram(const uint8_t *in, size_t n, uint32_t freqs[256]);
+/* decoded length of a stream (parses the framing on the host) */
+int32_t zr_fse_decompressed_size(const uint8_t *in, size_t n, size_t *out_len);
+/* device-resident: one coder lane per 0xF6 block (the only parallel unit the
+ * format has). *_dev status/out_len are device scalars. */
+size_t zr_fse_workspace_bytes(size_t n, const zr_fse_config *c);
+/* freqs_dev: device 256 x u32 raw frequency table, or NULL for the histogram of in */
+int32_t zr_fse_compress_dev(const zr_fse_config *c, const uint32_t *freqs_dev, const uint8_t *in,
+                            size_t n, uint8_t *out,
+                            uint64_t *out_len_dev, int32_t *status_dev, void *workspace,
+                            size_t workspace_bytes, void *stream);
+/* max_blocks: an upper bound of the stream's block count (the host knows it
+ * from the producer's config; zr_fse_decompressed_size parses it otherwise) */
+size_t zr_fse_decode_workspace_bytes(uint64_t max_blocks);
+int32_t zr_fse_decompress_dev(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                              uint64_t max_blocks, uint64_t *out_len_dev, int32_t *status_dev,
+                              void *workspace, size_t workspace_bytes, void *stream);
+
 /* ---- device memory helpers (for hosts without a HIP binding) ---- */
 int32_t zr_malloc_dev(void **ptr, size_t bytes);
 int32_t zr_free_dev(void *ptr);

@@ -470,6 +470,11 @@ size_t or_fse_compress_bound(size_t n, const or_fse_config *c) {
  * merge_compressed_blocks fse.rs:1026-1044. */
 int or_fse_compress(const or_fse_config *c, const uint8_t *in, size_t n, uint8_t *out,
                     size_t *out_len) {
+    return or_fse_compress_freqs(c, NULL, in, n, out, out_len);
+}
+
+int or_fse_compress_freqs(const or_fse_config *c, const uint32_t *freqs, const uint8_t *in, size_t n,
+                          uint8_t *out, size_t *out_len) {
     int st = fse_validate(c); /* FseEncoder::new, fse.rs:773-786 */
     if (st) return st;
     if (n == 0) {
@@ -477,7 +482,9 @@ int or_fse_compress(const or_fse_config *c, const uint8_t *in, size_t n, uint8_t
         return OK;
     }
     uint32_t hist[256] = {0};
-    for (size_t i = 0; i < n; i++) hist[in[i]]++; /* analyze_frequencies fse.rs:796-851 */
+    if (freqs) memcpy(hist, freqs, sizeof(hist));
+    else
+        for (size_t i = 0; i < n; i++) hist[in[i]]++; /* analyze_frequencies fse.rs:796-851 */
     fse_table *t = (fse_table *)malloc(sizeof(fse_table));
     st = fse_table_new(hist, t);
     if (st) {

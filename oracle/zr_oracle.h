@@ -56,6 +56,11 @@ int or_fse_normalize_exact(const uint32_t f[256], uint32_t table_size, uint32_t 
 size_t or_fse_compress_bound(size_t n, const or_fse_config *c);
 int or_fse_compress(const or_fse_config *c, const uint8_t *in, size_t n, uint8_t *out,
                     size_t *out_len);                        /* FseEncoder::compress fse.rs:854 */
+/* compress with a caller-given raw frequency table: the static-table path
+ * (adaptive=false reuses the first table, fse.rs:860-862) and dictionaries
+ * (dictionary byte counts added, fse.rs:807-812). freqs == NULL: histogram of in. */
+int or_fse_compress_freqs(const or_fse_config *c, const uint32_t *freqs, const uint8_t *in, size_t n,
+                          uint8_t *out, size_t *out_len);
 /* FseDecoder::decompress fse.rs:1105. out_cap bounds the output; *out_len = produced. */
 int or_fse_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap, size_t *out_len);
 /* Decoded length of a stream without decoding (host-side sizing helper). */

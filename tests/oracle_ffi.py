@@ -58,6 +58,8 @@ def lib():
         L.or_fse_compress_bound.argtypes = [sz, ctypes.POINTER(FseConfig)]
         L.or_fse_compress_bound.restype = sz
         L.or_fse_compress.argtypes = [ctypes.POINTER(FseConfig), u8p, sz, u8p, ctypes.POINTER(sz)]
+        L.or_fse_compress_freqs.argtypes = [ctypes.POINTER(FseConfig), ctypes.POINTER(ctypes.c_uint32), u8p,
+                                            sz, u8p, ctypes.POINTER(sz)]
         L.or_fse_decompress.argtypes = [u8p, sz, u8p, sz, ctypes.POINTER(sz)]
         L.or_fse_decompressed_size.argtypes = [u8p, sz, ctypes.POINTER(sz)]
         L.or_fse_mul_hi.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
@@ -152,6 +154,16 @@ def fse_compress(data, config=None):
     out = _out(lib().or_fse_compress_bound(n, ctypes.byref(c)))
     ol = sz(0)
     _check(lib().or_fse_compress(ctypes.byref(c), b, n, out, ctypes.byref(ol)), "fse_compress")
+    return ctypes.string_at(out, ol.value)
+
+
+def fse_compress_freqs(data, freqs, config=None):
+    c = config or fse_config()
+    b, n = _buf(data)
+    out = _out(lib().or_fse_compress_bound(n, ctypes.byref(c)))
+    ol = sz(0)
+    _check(lib().or_fse_compress_freqs(ctypes.byref(c), (ctypes.c_uint32 * 256)(*freqs), b, n, out,
+                                       ctypes.byref(ol)), "fse_compress_freqs")
     return ctypes.string_at(out, ol.value)
 
 

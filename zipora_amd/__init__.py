@@ -19,4 +19,7 @@ def synth(kind, n, seed=0):
     buf = (ctypes.c_uint8 * max(1, n))()
     from .errors import check
     check(load().zr_synth_fill(k, seed, buf, n))
-    return bytes(buf[:n])
+    return ctypes.string_at(buf, n)
+from .fse import (EntropyStats, FseConfig, FseDecoder, FseDevice, FseEncoder,  # noqa: F401,E402
+                  fse_compress, fse_compress_with_config, fse_decompress, fse_decompress_with_config,
+                  fse_unzip, fse_zip)

@@ -64,6 +64,21 @@ SIGNATURES = [
                                                   c_vp]),
     ("zr_rans_decode_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp, c_sz,
                                                   c_vp]),
+    ("zr_fse_config_default", None, [ctypes.POINTER(FseConfig)]),
+    ("zr_fse_compress_bound", c_sz, [c_sz, ctypes.POINTER(FseConfig)]),
+    ("zr_fse_compress", ctypes.c_int32, [ctypes.POINTER(FseConfig), c_u8p, c_sz, c_u8p, c_sz,
+                                         ctypes.POINTER(c_sz)]),
+    ("zr_fse_decompress", ctypes.c_int32, [c_u8p, c_sz, c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_fse_decompressed_size", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_fse_workspace_bytes", c_sz, [c_sz, ctypes.POINTER(FseConfig)]),
+    ("zr_fse_compress_dev", ctypes.c_int32, [ctypes.POINTER(FseConfig), c_vp, c_vp, c_sz, c_vp, c_vp,
+                                             c_vp, c_vp, c_sz, c_vp]),
+    ("zr_fse_compress_freqs", ctypes.c_int32, [ctypes.POINTER(FseConfig), c_u32p, c_u8p, c_sz, c_u8p,
+                                               c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_byte_histogram", ctypes.c_int32, [c_u8p, c_sz, c_u32p]),
+    ("zr_fse_decode_workspace_bytes", c_sz, [ctypes.c_uint64]),
+    ("zr_fse_decompress_dev", ctypes.c_int32, [c_vp, c_sz, c_vp, c_sz, ctypes.c_uint64, c_vp, c_vp,
+                                               c_vp, c_sz, c_vp]),
     ("zr_malloc_dev", ctypes.c_int32, [ctypes.POINTER(c_vp), c_sz]),
     ("zr_free_dev", ctypes.c_int32, [c_vp]),
     ("zr_memcpy_h2d", ctypes.c_int32, [c_vp, c_vp, c_sz, c_vp]),

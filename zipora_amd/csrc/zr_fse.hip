@@ -1,0 +1,982 @@
+// zr_fse.hip -- "FSE" (src/entropy/fse.rs) on MI355X / gfx950.
+//
+// The reference FSE is a ryg-style rANS64: 32-bit renormalisation words,
+// initial state 1, tables normalised to 4096 (fse.rs:411-735). Formats
+// (Appendix A):
+//   0xF5 | body                          (single serial chain)
+//   0xF6 | nblocks:u32 | size:u32 x nblocks | body x nblocks
+//   body = len:u32 | 0xFF | raw                      (len < 100)
+//        = len:u32 | 12 | nsym:u16 | (sym:u8, freq:u32) x nsym | words | state:u64
+// A body is ONE serial coder chain, so the only parallel unit is the 0xF6
+// block: one lane per block. The shared table lives in LDS.
+//
+// Encode: device histogram -> k_fse_tab (normalize_frequencies_exact,
+// init_enc_symbol with the portable wrapping mul_hi) -> k_fse_enc (lane per
+// block, words to 16-byte queued scratch stores) -> k_fse_scan (framing) ->
+// k_fse_compact (coalesced body assembly).
+// Decode: k_fse_frame -> k_fse_parse (one workgroup per block; dedupes tables
+// whose header bytes equal block 0's) -> k_fse_tabs -> k_fse_dec (lane per
+// block) .
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "zr_internal.h"
+
+namespace zr {
+
+constexpr uint32_t FSE_MODE_SINGLE = 0xF5;    // fse.rs:15
+constexpr uint32_t FSE_MODE_PARALLEL = 0xF6;  // fse.rs:17
+
+struct alignas(16) FseDTab {
+    uint32_t status, nsym, max_symbol, hdr_len;  // hdr_len = 3 + 5 * nsym
+    uint32_t freq[256];                          // normalised (header content)
+    uint32_t start[256];
+    uint64_t rcp[256];                           // init_enc_symbol (fse.rs:583-615)
+    uint32_t shift[256];
+    uint32_t bias[256];
+    uint32_t cmpl[256];
+    uint8_t alias[4096];
+    uint8_t hdr[3 + 5 * 256];  // table_log(12) | nsym:u16 | (sym, freq:u32) pairs
+};
+
+// FseTable::mul_hi (fse.rs:618-628): the middle sum wraps in release builds.
+__device__ __forceinline__ uint64_t mul_hi_portable(uint64_t a, uint64_t b) {
+    const uint64_t a_lo = a & 0xFFFFFFFFull, a_hi = a >> 32;
+    const uint64_t b_lo = b & 0xFFFFFFFFull, b_hi = b >> 32;
+    const uint64_t x0 = b_lo * a_lo;
+    const uint64_t x1 = (b_lo * a_hi) + (b_hi * a_lo) + (x0 >> 32);
+    return (b_hi * a_hi) + (x1 >> 32);
+}
+
+__device__ __forceinline__ uint64_t blk_sum64(uint64_t v, unsigned long long *sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor((unsigned long long)v, d, 64);
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    const uint64_t t = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+    return t;
+}
+
+__device__ __forceinline__ uint64_t blk_excl_scan64(uint64_t v, unsigned long long *sh, uint64_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        unsigned long long t = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += t;
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    unsigned long long base = 0;
+    for (int i = 0; i < w; i++) base += sh[i];
+    if (total) *total = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+    return base + inc - v;
+}
+
+// FseTable::new for the 256 frequencies f (one per thread of a 256-thread
+// block): normalize_frequencies_exact (fse.rs:513-580), init_enc_symbol
+// (fse.rs:583-615), alias table and the header pair list (fse.rs:909-928).
+__device__ void fse_build_table(uint32_t f, FseDTab *d, unsigned long long *sh, uint32_t *norm_s,
+                                uint32_t *raw_s, unsigned long long *best) {
+    const uint32_t v = threadIdx.x;
+    raw_s[v] = f;
+    const uint64_t total = blk_sum64(f, sh);
+    if (total == 0) {  // "No symbols found in frequency table" (fse.rs:415-422)
+        if (v == 0) d->status = ZR_INVALID_INPUT;
+        return;
+    }
+    const uint32_t scaled = f ? (uint32_t)(((uint64_t)f * 4096) / total) : 0u;
+    uint32_t norm = f ? (scaled > 1 ? scaled : 1u) : 0u;
+    norm_s[v] = norm;
+    const uint64_t assigned = blk_sum64(norm, sh);
+    if (assigned > 4096) {
+        // repeatedly shrink the current largest (lowest index on ties) by
+        // min(excess, max - 1) (fse.rs:542-560)
+        uint64_t excess = assigned - 4096;
+        while (excess > 0) {
+            if (v == 0) *best = 0;
+            __syncthreads();
+            if (norm_s[v]) atomicMax(best, ((unsigned long long)norm_s[v] << 8) | (255 - v));
+            __syncthreads();
+            const unsigned long long bk = *best;
+            __syncthreads();
+            const uint32_t idx = 255 - (uint32_t)(bk & 0xFF), mv = (uint32_t)(bk >> 8);
+            const uint64_t take = excess < (uint64_t)(mv - 1) ? excess : (uint64_t)(mv - 1);
+            if (v == 0) norm_s[idx] -= (uint32_t)take;
+            excess -= take;
+            __syncthreads();
+            if (take == 0) break;  // unreachable for <= 256 symbols (guard against a hang)
+        }
+    } else if (assigned < 4096) {
+        // whole deficit to the largest raw frequency, lowest index on ties (fse.rs:561-573)
+        if (v == 0) *best = 0;
+        __syncthreads();
+        if (f) atomicMax(best, ((unsigned long long)f << 8) | (255 - v));
+        __syncthreads();
+        if (v == 0) norm_s[255 - (uint32_t)(*best & 0xFF)] += (uint32_t)(4096 - assigned);
+        __syncthreads();
+    }
+    norm = norm_s[v];
+    // max_symbol: last symbol with a raw frequency (fse.rs:415)
+    if (v == 0) *best = 0;
+    __syncthreads();
+    if (f) atomicMax(best, (unsigned long long)v + 1);
+    __syncthreads();
+    const uint32_t max_symbol = (uint32_t)*best - 1;
+    __syncthreads();
+    const uint32_t present = (norm > 0 && v <= max_symbol) ? 1u : 0u;
+    const uint32_t nf = present ? norm : 0u;
+    uint64_t tot;
+    const uint32_t start = (uint32_t)blk_excl_scan64(nf, sh, &tot);
+    const uint32_t rank = (uint32_t)blk_excl_scan64(present, sh, &tot);
+    const uint32_t nsym = (uint32_t)tot;
+    d->freq[v] = norm;
+    d->start[v] = start;
+    uint64_t rcp = 0;
+    uint32_t shift = 0, bias = 0, cmpl = 0;
+    if (present) {
+        cmpl = 4096 - nf;
+        if (nf < 2) {
+            rcp = ~0ull;
+            shift = 0;
+            bias = start + 4096 - 1;
+        } else {
+            uint32_t sh2 = 0;
+            while (nf > (1u << sh2)) sh2++;
+            const uint64_t x0 = nf - 1, x1 = 1ull << (sh2 + 31);
+            const uint64_t t1 = x1 / nf;
+            const uint64_t x0e = x0 + ((x1 % nf) << 32);
+            const uint64_t t0 = x0e / nf;
+            rcp = t0 + (t1 << 32);
+            shift = sh2 - 1;
+            bias = start;
+        }
+        for (uint32_t i = 0; i < nf; i++) d->alias[start + i] = (uint8_t)v;
+        uint8_t *e = d->hdr + 3 + 5 * rank;
+        e[0] = (uint8_t)v;
+        e[1] = (uint8_t)norm;
+        e[2] = (uint8_t)(norm >> 8);
+        e[3] = (uint8_t)(norm >> 16);
+        e[4] = (uint8_t)(norm >> 24);
+    }
+    d->rcp[v] = rcp;
+    d->shift[v] = shift;
+    d->bias[v] = bias;
+    d->cmpl[v] = cmpl;
+    if (v == 0) {
+        d->status = ZR_OK;
+        d->nsym = nsym;
+        d->max_symbol = max_symbol;
+        d->hdr_len = 3 + 5 * nsym;
+        d->hdr[0] = 12;  // table.table_log is always TF_SHIFT (fse.rs:491)
+        d->hdr[1] = (uint8_t)nsym;
+        d->hdr[2] = (uint8_t)(nsym >> 8);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fse_tab(const uint32_t *hist, FseDTab *d) {
+    __shared__ unsigned long long sh[4], best;
+    __shared__ uint32_t norm_s[256], raw_s[256];
+    fse_build_table(hist[threadIdx.x], d, sh, norm_s, raw_s, &best);
+}
+
+__global__ __launch_bounds__(256) void k_fse_hist(const uint8_t *in, uint64_t n, uint32_t *hist) {
+    __shared__ uint32_t h[4][257];
+    for (int i = threadIdx.x; i < 4 * 257; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t *mine = h[threadIdx.x >> 6];
+    const uint64_t chunk = 64 * 1024;
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
+    for (uint64_t i = lo + threadIdx.x * 4; i < hi; i += 1024) {
+        if (i + 4 <= hi && (((uintptr_t)(in + i)) & 3) == 0) {
+            const uint32_t wv = *reinterpret_cast<const uint32_t *>(in + i);
+            atomicAdd(&mine[wv & 0xFF], 1u);
+            atomicAdd(&mine[(wv >> 8) & 0xFF], 1u);
+            atomicAdd(&mine[(wv >> 16) & 0xFF], 1u);
+            atomicAdd(&mine[wv >> 24], 1u);
+        } else {
+            for (uint64_t j = i; j < i + 4 && j < hi; j++) atomicAdd(&mine[in[j]], 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t v = threadIdx.x;
+    const uint32_t s = h[0][v] + h[1][v] + h[2][v] + h[3][v];
+    if (s) atomicAdd(&hist[v], s);
+}
+
+struct FseEncArgs {
+    const uint8_t *in;
+    uint64_t n, bs, nb;  // block size, block count (nb == 1: single body over all of in)
+    const FseDTab *tab;
+    uint8_t *scratch;    // per block: words (emission order) at scratch + j * cap
+    uint64_t cap;
+    uint32_t *wlen;      // bytes of words per block
+    uint64_t *state;     // final state per block
+    uint64_t *body;      // body bytes per block
+    int32_t *status;
+};
+
+typedef unsigned fv4u __attribute__((ext_vector_type(4)));
+
+// compress_single_internal (fse.rs:887-966): reverse scan, renormalize_encode
+// (fse.rs:680-700) then encode_symbol (fse.rs:632-648), one lane per block.
+__global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
+    __shared__ uint64_t s_rcp[256];
+    __shared__ uint32_t s_f[256], s_shift[256], s_bias[256], s_cmpl[256];
+    for (int i = threadIdx.x; i < 256; i += 64) {
+        s_rcp[i] = a.tab->rcp[i];
+        s_f[i] = a.tab->freq[i];
+        s_shift[i] = a.tab->shift[i];
+        s_bias[i] = a.tab->bias[i];
+        s_cmpl[i] = a.tab->cmpl[i];
+    }
+    __syncthreads();
+    const uint64_t j = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (j >= a.nb || a.tab->status != ZR_OK) return;
+    const uint64_t lo = j * a.bs, len = min(a.bs, a.n - lo);
+    if (len < 100) {  // raw marker body (fse.rs:892-904)
+        a.wlen[j] = 0;
+        a.state[j] = 0;
+        a.body[j] = 5 + len;
+        return;
+    }
+    const uint8_t *in = a.in + lo;
+    uint32_t *out = reinterpret_cast<uint32_t *>(a.scratch + j * a.cap);
+    fv4u *out4 = reinterpret_cast<fv4u *>(out);
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0;
+    uint64_t nout = 0;
+    uint64_t x = 1;  // fse.rs:931
+    bool err = false;
+    // the lane's input is read backwards through a 16-byte register chunk
+    uint64_t ck = (len - 1) & ~15ull;  // offset of the loaded chunk
+    bool vec = ((((uintptr_t)in) & 15) == 0);
+    fv4u chunk = {0, 0, 0, 0};
+    auto load_chunk = [&](uint64_t off) {
+        if (vec && off + 16 <= len) {
+            chunk = *reinterpret_cast<const fv4u *>(in + off);
+        } else {
+            uint32_t wv[4] = {0, 0, 0, 0};
+            for (uint32_t t = 0; t < 16; t++)
+                if (off + t < len) wv[t >> 2] |= (uint32_t)in[off + t] << (8 * (t & 3));
+            chunk = fv4u{wv[0], wv[1], wv[2], wv[3]};
+        }
+    };
+    load_chunk(ck);
+    for (uint64_t i = len; i-- > 0;) {
+        if (i < ck) {
+            ck -= 16;
+            load_chunk(ck);
+        }
+        const uint32_t t = (uint32_t)(i - ck);
+        const uint32_t wsel = t >> 2;
+        const uint32_t wv = wsel == 0 ? chunk.x : wsel == 1 ? chunk.y : wsel == 2 ? chunk.z : chunk.w;
+        const uint32_t sym = (wv >> (8 * (t & 3))) & 0xFF;
+        const uint32_t f = s_f[sym];
+        // renormalize_encode: x_max = ((RANS_L >> 12) << 32) * freq = freq << 36
+        if (x >= ((uint64_t)f << 36)) {
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            q3 = (uint32_t)x;
+            nq++;
+            x >>= 32;
+            if (nq == 4) {
+                out4[nout >> 2] = fv4u{q0, q1, q2, q3};
+                nout += 4;
+                nq = 0;
+            }
+        }
+        if (f == 0) {  // encode_symbol returns None (fse.rs:946-953)
+            err = true;
+            break;
+        }
+        const uint64_t q = mul_hi_portable(x, s_rcp[sym]) >> s_shift[sym];
+        x = x + (uint64_t)s_bias[sym] + q * (uint64_t)s_cmpl[sym];
+    }
+    {
+        const uint32_t qs[4] = {q0, q1, q2, q3};
+        for (uint32_t i = 0; i < nq; i++) out[nout + i] = qs[4 - nq + i];
+        nout += nq;
+    }
+    if (err) *a.status = ZR_INVALID_INPUT;
+    a.wlen[j] = (uint32_t)(nout * 4);
+    a.state[j] = x;
+    a.body[j] = 4 + a.tab->hdr_len + nout * 4 + 8;
+}
+
+// framing: body offsets, sizes table and total length (fse.rs:877-883, :1026-1044)
+// mode: 0 = 0xF5 single, 1 = 0xF6 parallel, 2 = body only (parallel_blocks = Some(1) quirk)
+__global__ __launch_bounds__(256) void k_fse_scan(const uint64_t *body, uint64_t nb, int mode, uint8_t *out,
+                                                  uint64_t *boff, uint64_t *out_len, int32_t *status,
+                                                  const FseDTab *tab) {
+    __shared__ unsigned long long sh[4];
+    const uint64_t pre = mode == 1 ? 5 + 4 * nb : (mode == 0 ? 1 : 0);
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nb; base += 256) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t v = i < nb ? body[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = blk_excl_scan64(v, sh, &tot);
+        if (i < nb) {
+            boff[i] = pre + carry + ex;
+            if (mode == 1) {
+                uint8_t *p = out + 5 + 4 * i;
+                p[0] = (uint8_t)v;
+                p[1] = (uint8_t)(v >> 8);
+                p[2] = (uint8_t)(v >> 16);
+                p[3] = (uint8_t)(v >> 24);
+            }
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        if (mode == 0) out[0] = FSE_MODE_SINGLE;
+        if (mode == 1) {
+            out[0] = FSE_MODE_PARALLEL;
+            out[1] = (uint8_t)nb;
+            out[2] = (uint8_t)(nb >> 8);
+            out[3] = (uint8_t)(nb >> 16);
+            out[4] = (uint8_t)(nb >> 24);
+        }
+        if (tab->status != ZR_OK) *status = tab->status;
+        *out_len = *status == ZR_OK ? pre + carry : 0;
+    }
+}
+
+// body assembly: len | header | words | state, or len | FF | raw. One
+// workgroup per block; the words are moved as aligned 16-byte destination units.
+__global__ __launch_bounds__(256) void k_fse_compact(FseEncArgs a, uint8_t *out, const uint64_t *boff) {
+    const uint64_t j = blockIdx.x;
+    if (j >= a.nb || *a.status != ZR_OK) return;
+    const uint64_t lo = j * a.bs, len = min(a.bs, a.n - lo);
+    uint8_t *dst = out + boff[j];
+    if (threadIdx.x < 4) dst[threadIdx.x] = (uint8_t)(len >> (8 * threadIdx.x));
+    if (len < 100) {
+        if (threadIdx.x == 0) dst[4] = 0xFF;
+        for (uint64_t i = threadIdx.x; i < len; i += 256) dst[5 + i] = a.in[lo + i];
+        return;
+    }
+    const uint32_t hl = a.tab->hdr_len;
+    for (uint32_t i = threadIdx.x; i < hl; i += 256) dst[4 + i] = a.tab->hdr[i];
+    const uint64_t W = a.wlen[j];
+    uint8_t *wd = dst + 4 + hl;
+    const uint8_t *src = a.scratch + j * a.cap;
+    const uintptr_t ua0 = ((uintptr_t)wd) & ~(uintptr_t)15;
+    const uint64_t nunits = ((uintptr_t)wd + W - ua0 + 15) / 16;
+    for (uint64_t u = threadIdx.x; u < nunits; u += 256) {
+        const uintptr_t ua = ua0 + 16 * u;
+        const int64_t o = (int64_t)(ua - (uintptr_t)wd);
+        if (o >= 0 && (uint64_t)o + 16 <= W) {
+            const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src + (o & ~(int64_t)3));
+            const uint32_t r = (uint32_t)(o & 3) * 8;
+            const uint32_t w0 = s4[0], w1 = s4[1], w2 = s4[2], w3 = s4[3], w4 = s4[4];
+            uint4 v;
+            v.x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> r);
+            v.y = (uint32_t)((((uint64_t)w2 << 32) | w1) >> r);
+            v.z = (uint32_t)((((uint64_t)w3 << 32) | w2) >> r);
+            v.w = (uint32_t)((((uint64_t)w4 << 32) | w3) >> r);
+            *reinterpret_cast<uint4 *>(ua) = v;
+        } else {
+            for (int t = 0; t < 16; t++) {
+                const int64_t p = o + t;
+                if (p >= 0 && (uint64_t)p < W) reinterpret_cast<uint8_t *>(ua)[t] = src[p];
+            }
+        }
+    }
+    if (threadIdx.x < 8) wd[W + threadIdx.x] = (uint8_t)(a.state[j] >> (8 * threadIdx.x));
+}
+
+// ---------------------------------------------------------------- decode
+struct FseBlk {         // parsed block
+    uint64_t body;      // offset of the body in the stream
+    uint64_t blen;      // body length
+    uint64_t orig;      // decoded length
+    uint64_t words;     // offset of the word area in the stream
+    uint64_t wbytes;    // word area length
+    uint64_t state;
+    uint32_t raw, table;  // raw body; table index (0 = shared with block 0)
+};
+
+struct FseDecArgs {
+    const uint8_t *in;
+    uint64_t n, max_blocks, out_cap;
+    uint8_t *out;
+    uint64_t *nblocks;  // device scalar
+    FseBlk *blk;
+    uint32_t *freqs;    // [max_blocks][256] raw header frequencies (table builds)
+    FseDTab *tabs;      // [max_blocks] (only built where blk.table == index)
+    uint64_t *ooff;     // output offset per block
+    uint64_t *out_len;
+    int32_t *status;
+};
+
+__device__ __forceinline__ uint32_t rd32(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ uint64_t rd64(const uint8_t *p) { return rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+
+// mode byte, block count and body offsets (FseDecoder::decompress fse.rs:1105-1148,
+// decompress_parallel fse.rs:1284-1312)
+__global__ __launch_bounds__(256) void k_fse_frame(FseDecArgs a) {
+    __shared__ unsigned long long sh[4];
+    __shared__ int s_mode;
+    __shared__ uint64_t s_nb;
+    const uint8_t *in = a.in;
+    const uint64_t n = a.n;
+    if (threadIdx.x == 0) {
+        int mode = -1;
+        uint64_t nb = 0;
+        if (n == 0) {
+            mode = 0;  // empty -> empty output
+        } else if (in[0] == FSE_MODE_SINGLE) {
+            mode = 1;
+            nb = 1;
+        } else if (in[0] == FSE_MODE_PARALLEL) {
+            if (n - 1 < 4) {
+                mode = -1;  // "truncated before block count"
+            } else {
+                nb = rd32(in + 1);
+                if (nb == 0 || nb > (n - 1 - 4) / 4) mode = -1;  // zero blocks / claims too many
+                else if (nb > a.max_blocks) mode = -2;
+                else mode = 2;
+            }
+        }  // else: unknown mode byte
+        s_mode = mode;
+        s_nb = nb;
+        *a.status = mode == -1 ? ZR_INVALID_INPUT : (mode == -2 ? ZR_UNSUPPORTED : ZR_OK);
+        *a.nblocks = mode > 0 ? nb : 0;
+        if (mode == 1) {
+            a.blk[0].body = 1;
+            a.blk[0].blen = n - 1;
+        }
+    }
+    __syncthreads();
+    if (s_mode != 2) return;
+    const uint64_t nb = s_nb;
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nb; base += 256) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t v = i < nb ? rd32(in + 5 + 4 * i) : 0;
+        uint64_t tot;
+        const uint64_t ex = blk_excl_scan64(v, sh, &tot);
+        if (i < nb) {
+            a.blk[i].body = 5 + 4 * nb + carry + ex;
+            a.blk[i].blen = v;
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0 && 5 + 4 * nb + carry > n) *a.status = ZR_INVALID_INPUT;  // "Invalid block data"
+}
+
+// decompress_single header parsing (fse.rs:1151-1249), one workgroup per block
+__global__ __launch_bounds__(256) void k_fse_parse(FseDecArgs a) {
+    const uint64_t j = blockIdx.x;
+    __shared__ int s_go;
+    // other workgroups of this grid may flip *status: read it once per workgroup
+    if (threadIdx.x == 0) s_go = j < *a.nblocks && *a.status == ZR_OK;
+    __syncthreads();
+    if (!s_go) return;
+    __shared__ int s_err, s_diff;
+    __shared__ uint32_t s_nsym, s_last[256];
+    const uint8_t *d = a.in + a.blk[j].body;
+    const uint64_t len = a.blk[j].blen;
+    FseBlk &B = a.blk[j];
+    if (threadIdx.x == 0) {
+        int err = 0;
+        B.raw = 0;
+        B.orig = 0;
+        B.wbytes = 0;
+        B.table = 0;
+        s_nsym = 0;
+        if (len == 0) {
+            B.raw = 2;  // empty body -> empty output
+        } else if (len < 5) {
+            err = 1;  // "Data too short for FSE header"
+        } else {
+            const uint64_t orig = rd32(d);
+            if (orig == 0) {
+                B.raw = 2;
+            } else if (d[4] == 0xFF) {
+                if (5 + orig > len) err = 1;  // "Incomplete uncompressed data"
+                B.raw = 1;
+                B.orig = orig;
+            } else if (d[4] < 5 || d[4] > 15) {
+                err = 1;  // "Invalid table log"
+            } else if (7 > len) {
+                err = 1;  // "Missing frequency table size"
+            } else {
+                const uint32_t nsym = (uint32_t)d[5] | ((uint32_t)d[6] << 8);
+                if (nsym == 0) err = 1;  // all-zero table: "No symbols found"
+                else if (7 + 5 * (uint64_t)nsym > len) err = 1;  // "Incomplete frequency table"
+                else if (7 + 5 * (uint64_t)nsym + 8 > len) err = 1;  // "Missing final state"
+                else {
+                    s_nsym = nsym;
+                    B.orig = orig;
+                    const uint64_t ss = len - 8;
+                    uint64_t st = rd64(d + ss);
+                    if (st == 0) st = 1;  // fse.rs:1247-1249
+                    B.state = st;
+                    B.words = a.blk[j].body + 7 + 5 * (uint64_t)nsym;
+                    B.wbytes = ss - (7 + 5 * (uint64_t)nsym);
+                }
+            }
+        }
+        s_err = err;
+        s_diff = 0;
+        if (err) *a.status = ZR_INVALID_INPUT;
+    }
+    __syncthreads();
+    if (s_err || s_nsym == 0) return;  // raw / empty / error: no table
+    const uint32_t nsym = s_nsym;
+    // same pair bytes as block 0 -> share table 0
+    if (j != 0) {
+        // block 0's header is re-read from the stream (its FseBlk is being
+        // written by another workgroup of this grid). Sharing needs a coded
+        // block 0 whose pair list is complete; any block-0 error fails the
+        // whole stream anyway.
+        const uint8_t *d0 = a.in + a.blk[0].body;
+        const uint64_t len0 = a.blk[0].blen;
+        const bool comparable = len0 >= 7 && rd32(d0) != 0 && d0[4] != 0xFF && d0[5] == d[5] &&
+                                d0[6] == d[6] && 7 + 5 * (uint64_t)nsym <= len0;
+        if (!comparable) {
+            if (threadIdx.x == 0) s_diff = 1;
+        } else {
+            for (uint32_t i = threadIdx.x; i < 5 * nsym; i += 256)
+                if (d0[7 + i] != d[7 + i]) s_diff = 1;
+        }
+        __syncthreads();
+        if (!s_diff) return;
+    }
+    if (threadIdx.x == 0) B.table = (uint32_t)j;
+    // raw frequencies: later entries for the same symbol win (fse.rs:1200-1215)
+    s_last[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nsym; i += 256) atomicMax(&s_last[d[7 + 5 * i]], i + 1);
+    __syncthreads();
+    const uint32_t li = s_last[threadIdx.x];
+    a.freqs[j * 256 + threadIdx.x] = li ? rd32(d + 7 + 5 * (li - 1) + 1) : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_fse_tabs(FseDecArgs a) {
+    const uint64_t j = blockIdx.x;
+    __shared__ int s_go;
+    if (threadIdx.x == 0) {
+        s_go = j < *a.nblocks && *a.status == ZR_OK;
+        if (s_go) {
+            const FseBlk &B = a.blk[j];
+            s_go = !(B.raw || B.table != j || B.orig == 0);
+        }
+    }
+    __syncthreads();
+    if (!s_go) return;
+    __shared__ unsigned long long sh[4], best;
+    __shared__ uint32_t norm_s[256], raw_s[256];
+    fse_build_table(a.freqs[j * 256 + threadIdx.x], &a.tabs[j], sh, norm_s, raw_s, &best);
+    __syncthreads();
+    if (threadIdx.x == 0 && a.tabs[j].status != ZR_OK) *a.status = ZR_INVALID_INPUT;
+}
+
+__global__ __launch_bounds__(256) void k_fse_outscan(FseDecArgs a) {
+    __shared__ unsigned long long sh[4];
+    if (*a.status != ZR_OK) {
+        if (threadIdx.x == 0) *a.out_len = 0;
+        return;
+    }
+    const uint64_t nb = *a.nblocks;
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nb; base += 256) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t v = i < nb ? a.blk[i].orig : 0;
+        uint64_t tot;
+        const uint64_t ex = blk_excl_scan64(v, sh, &tot);
+        if (i < nb) a.ooff[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        *a.out_len = carry;
+        if (carry > a.out_cap) *a.status = ZR_INVALID_INPUT;  // output buffer too small
+    }
+}
+
+// decode loop of decompress_single (fse.rs:1258-1278): decode_symbol
+// (fse.rs:664-676) then renormalize_decode (fse.rs:704-735). One lane per block.
+__global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
+    __shared__ uint8_t s_alias[4096];
+    __shared__ uint32_t s_fs[256];  // freq | start << 16
+    const uint64_t j = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    const uint64_t nb = *a.nblocks;
+    const bool ok = *a.status == ZR_OK;
+    // table 0 into LDS when any block uses it
+    const FseDTab *T0 = &a.tabs[0];
+    const bool t0 = ok && nb > 0 && a.blk[0].raw == 0 && a.blk[0].orig > 0;
+    if (t0) {
+        for (int i = threadIdx.x; i < 1024; i += 64)
+            reinterpret_cast<uint32_t *>(s_alias)[i] = reinterpret_cast<const uint32_t *>(T0->alias)[i];
+        for (int i = threadIdx.x; i < 256; i += 64) s_fs[i] = T0->freq[i] | (T0->start[i] << 16);
+    }
+    __syncthreads();
+    if (!ok || j >= nb) return;
+    const FseBlk B = a.blk[j];
+    uint8_t *out = a.out + a.ooff[j];
+    if (B.raw == 2 || B.orig == 0) return;
+    if (B.raw == 1) {
+        const uint8_t *src = a.in + B.body + 5;
+        for (uint64_t i = 0; i < B.orig; i++) out[i] = src[i];
+        return;
+    }
+    const bool shared = B.table == 0;
+    const FseDTab *T = &a.tabs[B.table];
+    const uint8_t *wd = a.in + B.words;
+    uint64_t bp = B.wbytes;
+    uint64_t x = B.state;
+    const bool vec = ((((uintptr_t)out) & 15) == 0);
+    // 16-byte output queue: acc collects 4 symbols, w0..w2 the completed
+    // dwords of the current 16-byte group.
+    uint32_t w0 = 0, w1 = 0, w2 = 0, acc = 0;
+    for (uint64_t i = 0; i < B.orig; i++) {
+        const uint32_t lo = (uint32_t)(x & 4095);
+        uint32_t s, f, st;
+        if (shared) {
+            s = s_alias[lo];
+            const uint32_t fs = s_fs[s];
+            f = fs & 0xFFFF;
+            st = fs >> 16;
+        } else {
+            s = T->alias[lo];
+            f = T->freq[s];
+            st = T->start[s];
+        }
+        x = (uint64_t)f * (x >> 12) + lo - st;
+        if (vec) {
+            acc = (acc >> 8) | (s << 24);
+            if ((i & 15) == 15) {
+                *reinterpret_cast<uint4 *>(out + i - 15) = make_uint4(w0, w1, w2, acc);
+            } else if ((i & 3) == 3) {
+                w0 = w1;
+                w1 = w2;
+                w2 = acc;
+            }
+        } else {
+            out[i] = (uint8_t)s;
+        }
+        if (x < 65536 && bp > 0) {
+            if (bp >= 4) {
+                bp -= 4;
+                x = (x << 32) | rd32(wd + bp);
+            } else {
+                bp -= 1;
+                x = (x << 8) | wd[bp];
+            }
+        }
+        if (x < 1) x = 1;
+    }
+    const uint32_t rem = (uint32_t)(B.orig & 15);
+    if (vec && rem) {
+        // partial last group: c completed dwords in w(3-c)..w2, r bytes in acc's top
+        const uint64_t g = B.orig - rem;
+        const uint32_t c = rem >> 2, r = rem & 3;
+        const uint32_t ws[3] = {w0, w1, w2};
+        for (uint32_t k = 0; k < c; k++) *reinterpret_cast<uint32_t *>(out + g + 4 * k) = ws[3 - c + k];
+        for (uint32_t t = 0; t < r; t++) out[g + 4 * c + t] = (uint8_t)(acc >> (8 * (4 - r + t)));
+    }
+}
+
+size_t fse_dec_ws_bytes(uint64_t maxb) {
+    return 256 + round_up(sizeof(FseBlk) * maxb, 256) + round_up(4ull * 256 * maxb, 256) +
+           round_up(sizeof(FseDTab) * maxb, 256) + round_up(8 * maxb, 256) + 256;
+}
+
+struct FsePlan {
+    uint64_t nb, bs;
+    int mode;  // 0 F5, 1 F6, 2 body only
+};
+static FsePlan fse_plan(const zr_fse_config *c, uint64_t n) {
+    FsePlan p;
+    if (c->parallel_blocks != 0 && c->block_size > 0 && n > c->block_size * 2) {
+        p.bs = c->block_size;
+        p.nb = (n + p.bs - 1) / p.bs;
+        p.mode = c->parallel_blocks <= 1 ? 2 : 1;  // Some(1): single body, no mode byte (fse.rs:975-977)
+        if (p.mode == 2) {
+            p.nb = 1;
+            p.bs = n;
+        }
+    } else {
+        p.bs = n;
+        p.nb = 1;
+        p.mode = 0;
+    }
+    return p;
+}
+
+static int32_t fse_validate(const zr_fse_config *c) {  // FseConfig::validate (fse.rs:317-348)
+    if (c->table_log < 5 || c->table_log > 15) return set_error(ZR_INVALID_INPUT, "Table log must be 5-15");
+    if (c->compression_level < 1 || c->compression_level > 22)
+        return set_error(ZR_INVALID_INPUT, "Compression level must be 1-22");
+    if ((1ull << c->table_log) > c->max_table_size) return set_error(ZR_INVALID_INPUT, "Table size exceeds max");
+    return ZR_OK;
+}
+
+static uint64_t fse_cap(uint64_t bs) { return round_up(bs + bs / 2 + 64, 16); }
+
+}  // namespace zr
+
+using namespace zr;
+
+extern "C" {
+
+void zr_fse_config_default(zr_fse_config *c) {
+    c->table_log = 12;
+    c->compression_level = 3;
+    c->max_table_size = 64 * 1024;
+    c->parallel_blocks = 0;
+    c->block_size = 64 * 1024;
+    c->adaptive = 1;
+}
+
+size_t zr_fse_compress_bound(size_t n, const zr_fse_config *c) {
+    const FsePlan p = fse_plan(c, n);
+    // per block: len + header(3 + 5*256) + words (<= 1.5 B/symbol) + state, + framing
+    return n + n / 2 + p.nb * (4 + 3 + 5 * 256 + 8 + 4 + 16) + 64;
+}
+
+size_t zr_fse_workspace_bytes(size_t n, const zr_fse_config *c) {
+    const FsePlan p = fse_plan(c, n);
+    return 1024 + round_up(sizeof(FseDTab), 256) + round_up(p.nb * fse_cap(p.bs), 256) +
+           round_up(4 * p.nb, 256) + 3 * round_up(8 * p.nb, 256) + 512;
+}
+
+int32_t zr_fse_compress_dev(const zr_fse_config *c, const uint32_t *freqs_dev, const uint8_t *in, size_t n,
+                            uint8_t *out, uint64_t *out_len_dev, int32_t *status_dev, void *ws, size_t ws_bytes,
+                            void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    int32_t st = fse_validate(c);  // FseEncoder::new (fse.rs:773-786)
+    if (st) return st;
+    hipStream_t s = (hipStream_t)stream;
+    ZR_HIP(hipMemsetAsync(status_dev, 0, 4, s));
+    if (n == 0) {  // empty input -> empty output (fse.rs:855-857)
+        ZR_HIP(hipMemsetAsync(out_len_dev, 0, 8, s));
+        return ZR_OK;
+    }
+    if (ws_bytes < zr_fse_workspace_bytes(n, c)) return set_error(ZR_INVALID_INPUT, "FSE workspace too small");
+    const FsePlan p = fse_plan(c, n);
+    uint8_t *w = reinterpret_cast<uint8_t *>(round_up((uintptr_t)ws, 256));
+    uint32_t *hist = reinterpret_cast<uint32_t *>(w);
+    w += 1024;
+    FseDTab *tab = reinterpret_cast<FseDTab *>(w);
+    w += round_up(sizeof(FseDTab), 256);
+    FseEncArgs a;
+    a.in = in;
+    a.n = n;
+    a.bs = p.bs;
+    a.nb = p.nb;
+    a.tab = tab;
+    a.cap = fse_cap(p.bs);
+    a.scratch = w;
+    w += round_up(p.nb * a.cap, 256);
+    a.wlen = reinterpret_cast<uint32_t *>(w);
+    w += round_up(4 * p.nb, 256);
+    a.state = reinterpret_cast<uint64_t *>(w);
+    w += round_up(8 * p.nb, 256);
+    a.body = reinterpret_cast<uint64_t *>(w);
+    w += round_up(8 * p.nb, 256);
+    uint64_t *boff = reinterpret_cast<uint64_t *>(w);
+    a.status = status_dev;
+    if (freqs_dev) {
+        hist = const_cast<uint32_t *>(freqs_dev);
+    } else {
+        ZR_HIP(hipMemsetAsync(hist, 0, 1024, s));
+        timer_begin("fse_histogram", s);
+        hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, 64 * 1024)), dim3(256), 0, s, in, (uint64_t)n,
+                           hist);
+        timer_end("fse_histogram", s);
+    }
+    hipLaunchKernelGGL(k_fse_tab, dim3(1), dim3(256), 0, s, hist, tab);
+    timer_begin("fse_encode", s);
+    hipLaunchKernelGGL(k_fse_enc, dim3((uint32_t)ceil_div(p.nb, 64)), dim3(64), 0, s, a);
+    timer_end("fse_encode", s);
+    hipLaunchKernelGGL(k_fse_scan, dim3(1), dim3(256), 0, s, a.body, p.nb, p.mode, out, boff, out_len_dev,
+                       status_dev, tab);
+    hipLaunchKernelGGL(k_fse_compact, dim3((uint32_t)p.nb), dim3(256), 0, s, a, out, boff);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+size_t zr_fse_decode_workspace_bytes(uint64_t max_blocks) { return fse_dec_ws_bytes(max_blocks ? max_blocks : 1); }
+
+int32_t zr_fse_decompress_dev(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap, uint64_t max_blocks,
+                              uint64_t *out_len_dev, int32_t *status_dev, void *ws, size_t ws_bytes,
+                              void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (max_blocks == 0) max_blocks = 1;
+    if (ws_bytes < fse_dec_ws_bytes(max_blocks)) return set_error(ZR_INVALID_INPUT, "FSE workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    uint8_t *w = reinterpret_cast<uint8_t *>(round_up((uintptr_t)ws, 256));
+    FseDecArgs a;
+    a.in = in;
+    a.n = n;
+    a.max_blocks = max_blocks;
+    a.out_cap = out_cap;
+    a.out = out;
+    a.nblocks = reinterpret_cast<uint64_t *>(w);
+    w += 256;
+    a.blk = reinterpret_cast<FseBlk *>(w);
+    w += round_up(sizeof(FseBlk) * max_blocks, 256);
+    a.freqs = reinterpret_cast<uint32_t *>(w);
+    w += round_up(4ull * 256 * max_blocks, 256);
+    a.tabs = reinterpret_cast<FseDTab *>(w);
+    w += round_up(sizeof(FseDTab) * max_blocks, 256);
+    a.ooff = reinterpret_cast<uint64_t *>(w);
+    a.out_len = out_len_dev;
+    a.status = status_dev;
+    const uint32_t gb = (uint32_t)max_blocks;
+    hipLaunchKernelGGL(k_fse_frame, dim3(1), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_fse_parse, dim3(gb), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_fse_tabs, dim3(gb), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_fse_outscan, dim3(1), dim3(256), 0, s, a);
+    timer_begin("fse_decode", s);
+    hipLaunchKernelGGL(k_fse_dec, dim3((uint32_t)ceil_div(max_blocks, 64)), dim3(64), 0, s, a);
+    timer_end("fse_decode", s);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+// ---- host-memory entry points (synchronous)
+namespace {
+struct DBuf {
+    void *p = nullptr;
+    ~DBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+}  // namespace
+
+int32_t zr_fse_decompressed_size(const uint8_t *in, size_t n, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    *out_len = 0;
+    if (n == 0) return ZR_OK;
+    auto body_size = [&](const uint8_t *d, size_t len) -> size_t {
+        if (len < 5) return 0;
+        return (size_t)d[0] | ((size_t)d[1] << 8) | ((size_t)d[2] << 16) | ((size_t)d[3] << 24);
+    };
+    if (in[0] == FSE_MODE_SINGLE) {
+        *out_len = body_size(in + 1, n - 1);
+        return ZR_OK;
+    }
+    if (in[0] != FSE_MODE_PARALLEL || n < 5) return set_error(ZR_INVALID_INPUT, "unknown FSE stream mode byte");
+    const size_t nb = (size_t)in[1] | ((size_t)in[2] << 8) | ((size_t)in[3] << 16) | ((size_t)in[4] << 24);
+    if (nb == 0 || nb > (n - 5) / 4) return set_error(ZR_INVALID_INPUT, "invalid FSE block count");
+    size_t pos = 5 + 4 * nb, tot = 0;
+    for (size_t b = 0; b < nb; b++) {
+        const uint8_t *q = in + 5 + 4 * b;
+        const size_t bs = (size_t)q[0] | ((size_t)q[1] << 8) | ((size_t)q[2] << 16) | ((size_t)q[3] << 24);
+        if (pos + bs > n) return set_error(ZR_INVALID_INPUT, "Invalid block data");
+        tot += body_size(in + pos, bs);
+        pos += bs;
+    }
+    *out_len = tot;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_fse_compress(const zr_fse_config *c, const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                        size_t *out_len) {
+    return zr_fse_compress_freqs(c, nullptr, in, n, out, out_cap, out_len);
+}
+
+int32_t zr_byte_histogram(const uint8_t *in, size_t n, uint32_t freqs[256]) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    memset(freqs, 0, 1024);
+    if (n == 0) return ZR_OK;
+    DBuf din, dh;
+    ZR_HIP(hipMalloc(&din.p, n));
+    ZR_HIP(hipMalloc(&dh.p, 1024));
+    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
+    ZR_HIP(hipMemset(dh.p, 0, 1024));
+    hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, 64 * 1024)), dim3(256), 0, nullptr,
+                       (const uint8_t *)din.p, (uint64_t)n, (uint32_t *)dh.p);
+    ZR_HIP(hipGetLastError());
+    ZR_HIP(hipMemcpy(freqs, dh.p, 1024, hipMemcpyDeviceToHost));
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_fse_compress_freqs(const zr_fse_config *c, const uint32_t *freqs, const uint8_t *in, size_t n,
+                              uint8_t *out, size_t out_cap, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    int32_t st = fse_validate(c);
+    if (st) return st;
+    *out_len = 0;
+    if (n == 0) return ZR_OK;
+    const size_t wsb = zr_fse_workspace_bytes(n, c), cap = zr_fse_compress_bound(n, c);
+    DBuf din, dout, dws, dm;
+    ZR_HIP(hipMalloc(&din.p, n));
+    ZR_HIP(hipMalloc(&dout.p, cap));
+    ZR_HIP(hipMalloc(&dws.p, wsb));
+    ZR_HIP(hipMalloc(&dm.p, 64 + 1024));
+    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
+    uint64_t *olen = reinterpret_cast<uint64_t *>(dm.p);
+    int32_t *dst = reinterpret_cast<int32_t *>(olen + 1);
+    uint32_t *dfreq = nullptr;
+    if (freqs) {
+        dfreq = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(dm.p) + 64);
+        ZR_HIP(hipMemcpy(dfreq, freqs, 1024, hipMemcpyHostToDevice));
+    }
+    st = zr_fse_compress_dev(c, dfreq, (const uint8_t *)din.p, n, (uint8_t *)dout.p, olen, dst, dws.p, wsb,
+                             nullptr);
+    if (st) return st;
+    ZR_HIP(hipDeviceSynchronize());
+    uint64_t meta[2];
+    ZR_HIP(hipMemcpy(meta, dm.p, 16, hipMemcpyDeviceToHost));
+    if ((int32_t)meta[1] != 0) return set_error(ZR_INVALID_INPUT, "FSE compression failed");
+    if (meta[0] > out_cap) return set_error(ZR_INVALID_INPUT, "output capacity too small");
+    ZR_HIP(hipMemcpy(out, dout.p, meta[0], hipMemcpyDeviceToHost));
+    *out_len = meta[0];
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_fse_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    *out_len = 0;
+    if (n == 0) return ZR_OK;
+    // block count bound from the framing (host side)
+    uint64_t maxb = 1;
+    if (in[0] == FSE_MODE_PARALLEL && n >= 5) {
+        const uint64_t nb = (uint64_t)in[1] | ((uint64_t)in[2] << 8) | ((uint64_t)in[3] << 16) | ((uint64_t)in[4] << 24);
+        if (nb <= (n - 5) / 4 && nb > 0) maxb = nb;
+    }
+    const size_t wsb = fse_dec_ws_bytes(maxb);
+    DBuf din, dout, dws, dm;
+    ZR_HIP(hipMalloc(&din.p, n));
+    ZR_HIP(hipMalloc(&dout.p, out_cap ? out_cap : 16));
+    ZR_HIP(hipMalloc(&dws.p, wsb));
+    ZR_HIP(hipMalloc(&dm.p, 64));
+    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
+    uint64_t *olen = reinterpret_cast<uint64_t *>(dm.p);
+    int32_t *dst = reinterpret_cast<int32_t *>(olen + 1);
+    int32_t st = zr_fse_decompress_dev((const uint8_t *)din.p, n, (uint8_t *)dout.p, out_cap, maxb, olen, dst,
+                                       dws.p, wsb, nullptr);
+    if (st) return st;
+    ZR_HIP(hipDeviceSynchronize());
+    uint64_t meta[2];
+    ZR_HIP(hipMemcpy(meta, dm.p, 16, hipMemcpyDeviceToHost));
+    if ((int32_t)meta[1] != 0) return set_error((int32_t)meta[1], "FSE decompression failed: invalid data");
+    if (meta[0]) ZR_HIP(hipMemcpy(out, dout.p, meta[0], hipMemcpyDeviceToHost));
+    *out_len = meta[0];
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+}  // extern "C"

@@ -5,9 +5,11 @@ from . import _lib
 class ZiporaError(Exception):
     """Raised for any non-zero C ABI status; .code is the CResult value (src/ffi/mod.rs:29-58)."""
 
-    def __init__(self, code, message):
+    def __init__(self, code_or_message, message=None):
+        if message is None:  # ZiporaError("...") == invalid data / parameter
+            code_or_message, message = _lib.ZR_INVALID_INPUT, code_or_message
         super().__init__(message)
-        self.code = code
+        self.code = code_or_message
 
     @property
     def is_invalid_data(self):
