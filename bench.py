@@ -36,6 +36,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--workload", default="rans", choices=["rans", "fse"],
+                   help="rans = BASELINE metric (configs[1]); fse = configs[2] (secondary line)")
+    p.add_argument("--fse-block-kib", type=int, default=64)
     return p.parse_args()
 
 
@@ -73,6 +76,109 @@ def _table_fast(O, d):
     return O.rans_table([int(x) for x in h])
 
 
+def kernel_ms(L, name):
+    ms, cnt = ctypes.c_double(0), ctypes.c_uint64(0)
+    L.zr_timer_read(name.encode(), ctypes.byref(ms), ctypes.byref(cnt))
+    return ms.value / max(1, cnt.value), cnt.value
+
+
+def cpu_baseline_fse(host, bs, threads):
+    """The oracle (C restatement of src/entropy/fse.rs, 'port'): FSE 0xF6
+    compress+decompress on bounded slices, slices spread over threads."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import concurrent.futures as cf
+    import oracle_ffi as O
+    O.lib()
+    sl = 8 << 20
+    ns = min(len(host) // sl, 2 * threads)
+    cfg = O.fse_config(parallel_blocks=8, block_size=bs)
+
+    def one(i):
+        d = host[i * sl:(i + 1) * sl]
+        enc = O.fse_compress(d, cfg)
+        assert O.fse_decompress(enc, len(d)) == d
+        return len(enc)
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(one, range(ns)))
+    dt = time.perf_counter() - t0
+    return {"value": round(ns * sl / 2**30 / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{ns} x 8 MiB slices of the same Zipf workload, each an independent 0xF6 stream "
+                      f"(Some(8), {bs >> 10} KiB blocks), compress+decompress, {threads} threads, {dt:.2f} s"}
+
+
+def run_fse(args, torch, dist, world, rank, dev, zr, L):
+    """configs[2]: FSE encode+decode, 256 MiB Zipf(1.1) per GPU, 0xF6 blocks (Some(8))."""
+    total = 256 << 20
+    bs = args.fse_block_kib << 10
+    host = zr.synth("z", total, seed=0x9E3779B97F4A7C15 + rank)
+    raw = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+    cfg = zr.FseConfig(parallel_blocks=8, block_size=bs)
+    fd = zr.FseDevice(cfg, max_len=total, device=dev)
+    enc = torch.empty(fd.bound(total), dtype=torch.uint8, device=dev)
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    nblk = fd.n_blocks(total)
+    fd2 = zr.FseDevice(cfg, device=dev)  # separate meta for decode
+    cap = enc.numel()
+
+    def step():
+        fd.compress_async(raw, enc)
+        fd2.decompress_async(enc, cap, out, nblk)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    clen, st = fd.result()
+    dlen, st2 = fd2.result()
+    if st or st2 or dlen != total or not torch.equal(out, raw):
+        raise SystemExit(f"FSE warmup mismatch (status {st}/{st2}, len {dlen})")
+    L.zr_timer_reset()
+    L.zr_timer_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    L.zr_timer_enable(0)
+    dec_ms, _ = kernel_ms(L, "fse_decode")
+    enc_ms, _ = kernel_ms(L, "fse_encode")
+    hist_ms, _ = kernel_ms(L, "fse_histogram")
+    L.zr_timer_reset()
+    if not torch.equal(out, raw):
+        raise SystemExit("FSE decode mismatch in timed region")
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    dec_bytes = clen + total
+    achieved = dec_bytes / (dec_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
+    res = {
+        "metric": "GiB/s encode+decode (device-resident), FSE, 256 MiB Zipf(1.1), MI355X",
+        "value": round(world * total * args.steps / dt / 2**30, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (Zipf alpha=1.1 bytes, inverse CDF over the xorshift64 generator)",
+        "config": {"workload": f"FSE 0xF6 encode+decode, 256 MiB Zipf per GPU, parallel_blocks=Some(8), "
+                               f"block_size={bs >> 10} KiB ({nblk} blocks, one coder lane each)",
+                   "block_size": bs, "blocks": nblk, "parallelism": f"shard{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_fse_dec",
+                     "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
+        "kernels_ms": {"fse_decode": round(dec_ms, 4), "fse_encode": round(enc_ms, 4),
+                       "fse_histogram": round(hist_ms, 4)},
+        "compressed_bytes": clen, "ratio": round(clen / total, 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_fse(host, bs, args.cpu_threads)
+    return res
+
+
 def main():
     args = parse()
     import torch
@@ -90,6 +196,14 @@ def main():
     from zipora_amd.device import RansDeviceBatch
     L = zr.load()
     L.zr_set_device(local)
+
+    if args.workload == "fse":
+        res = run_fse(args, torch, dist, world, rank, dev, zr, L)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     B, n, N = args.buffers, args.buffer_mib << 20, args.streams
     total = B * n
@@ -132,9 +246,7 @@ def main():
     L.zr_timer_enable(0)
 
     def kt(name):
-        ms, cnt = ctypes.c_double(0), ctypes.c_uint64(0)
-        L.zr_timer_read(name.encode(), ctypes.byref(ms), ctypes.byref(cnt))
-        return ms.value / max(1, cnt.value), cnt.value
+        return kernel_ms(L, name)
 
     dec_ms, dec_n = kt("rans_decode")
     enc_ms, _ = kt("rans_encode")

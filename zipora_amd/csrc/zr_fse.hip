@@ -36,7 +36,10 @@ struct alignas(16) FseDTab {
     uint32_t shift[256];
     uint32_t bias[256];
     uint32_t cmpl[256];
-    uint8_t alias[4096];
+    // encode entry per symbol: {rcp lo, rcp hi, bias | cmpl << 16, freq | shift << 16}
+    uint4 enc[256];
+    // decode slot per state: sym | (freq - 1) << 8 | (slot - start) << 20
+    uint32_t slot[4096];
     uint8_t hdr[3 + 5 * 256];  // table_log(12) | nsym:u16 | (sym, freq:u32) pairs
 };
 
@@ -155,7 +158,7 @@ __device__ void fse_build_table(uint32_t f, FseDTab *d, unsigned long long *sh, 
             shift = sh2 - 1;
             bias = start;
         }
-        for (uint32_t i = 0; i < nf; i++) d->alias[start + i] = (uint8_t)v;
+        for (uint32_t i = 0; i < nf; i++) d->slot[start + i] = v | ((nf - 1) << 8) | (i << 20);
         uint8_t *e = d->hdr + 3 + 5 * rank;
         e[0] = (uint8_t)v;
         e[1] = (uint8_t)norm;
@@ -167,6 +170,7 @@ __device__ void fse_build_table(uint32_t f, FseDTab *d, unsigned long long *sh, 
     d->shift[v] = shift;
     d->bias[v] = bias;
     d->cmpl[v] = cmpl;
+    d->enc[v] = make_uint4((uint32_t)rcp, (uint32_t)(rcp >> 32), bias | (cmpl << 16), nf | (shift << 16));
     if (v == 0) {
         d->status = ZR_OK;
         d->nsym = nsym;
@@ -224,16 +228,12 @@ typedef unsigned fv4u __attribute__((ext_vector_type(4)));
 
 // compress_single_internal (fse.rs:887-966): reverse scan, renormalize_encode
 // (fse.rs:680-700) then encode_symbol (fse.rs:632-648), one lane per block.
+// The input is read backwards in aligned 16-byte chunks with two chunks of
+// prefetch; each chunk's 16 steps are unrolled so the LDS entry reads (which
+// depend only on the symbols) are off the state's dependency chain.
 __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
-    __shared__ uint64_t s_rcp[256];
-    __shared__ uint32_t s_f[256], s_shift[256], s_bias[256], s_cmpl[256];
-    for (int i = threadIdx.x; i < 256; i += 64) {
-        s_rcp[i] = a.tab->rcp[i];
-        s_f[i] = a.tab->freq[i];
-        s_shift[i] = a.tab->shift[i];
-        s_bias[i] = a.tab->bias[i];
-        s_cmpl[i] = a.tab->cmpl[i];
-    }
+    __shared__ uint4 s_e[256];
+    for (int i = threadIdx.x; i < 256; i += 64) s_e[i] = a.tab->enc[i];
     __syncthreads();
     const uint64_t j = (uint64_t)blockIdx.x * 64 + threadIdx.x;
     if (j >= a.nb || a.tab->status != ZR_OK) return;
@@ -251,51 +251,52 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
     uint64_t nout = 0;
     uint64_t x = 1;  // fse.rs:931
     bool err = false;
-    // the lane's input is read backwards through a 16-byte register chunk
-    uint64_t ck = (len - 1) & ~15ull;  // offset of the loaded chunk
-    bool vec = ((((uintptr_t)in) & 15) == 0);
-    fv4u chunk = {0, 0, 0, 0};
-    auto load_chunk = [&](uint64_t off) {
-        if (vec && off + 16 <= len) {
-            chunk = *reinterpret_cast<const fv4u *>(in + off);
-        } else {
-            uint32_t wv[4] = {0, 0, 0, 0};
-            for (uint32_t t = 0; t < 16; t++)
-                if (off + t < len) wv[t >> 2] |= (uint32_t)in[off + t] << (8 * (t & 3));
-            chunk = fv4u{wv[0], wv[1], wv[2], wv[3]};
-        }
-    };
-    load_chunk(ck);
-    for (uint64_t i = len; i-- > 0;) {
-        if (i < ck) {
-            ck -= 16;
-            load_chunk(ck);
-        }
-        const uint32_t t = (uint32_t)(i - ck);
-        const uint32_t wsel = t >> 2;
-        const uint32_t wv = wsel == 0 ? chunk.x : wsel == 1 ? chunk.y : wsel == 2 ? chunk.z : chunk.w;
-        const uint32_t sym = (wv >> (8 * (t & 3))) & 0xFF;
-        const uint32_t f = s_f[sym];
+    auto step_e = [&](const uint4 e) {
+        const uint32_t f = e.w & 0xFFFF;
+        err |= (f == 0);  // encode_symbol returns None (fse.rs:946-953)
         // renormalize_encode: x_max = ((RANS_L >> 12) << 32) * freq = freq << 36
-        if (x >= ((uint64_t)f << 36)) {
+        if (x >= ((uint64_t)(f ? f : 1u) << 36)) {
             q0 = q1;
             q1 = q2;
             q2 = q3;
             q3 = (uint32_t)x;
-            nq++;
             x >>= 32;
-            if (nq == 4) {
+            if (++nq == 4) {
                 out4[nout >> 2] = fv4u{q0, q1, q2, q3};
                 nout += 4;
                 nq = 0;
             }
         }
-        if (f == 0) {  // encode_symbol returns None (fse.rs:946-953)
-            err = true;
-            break;
+        const uint64_t rcp = ((uint64_t)e.y << 32) | e.x;
+        const uint64_t q = mul_hi_portable(x, rcp) >> (e.w >> 16);
+        x = x + (uint64_t)(e.z & 0xFFFF) + q * (uint64_t)(e.z >> 16);
+    };
+    auto step = [&](uint32_t sym) { step_e(s_e[sym]); };
+    const uint64_t full = len & ~15ull;
+    for (uint64_t i = len; i > full;) step(in[--i]);  // ragged top, < 16 symbols
+    if (full && !err) {
+        int64_t c = (int64_t)(full >> 4) - 1;
+        if ((((uintptr_t)in) & 15) == 0) {
+            const fv4u *in4 = reinterpret_cast<const fv4u *>(in);
+            const fv4u z = {0, 0, 0, 0};
+            fv4u cur = in4[c];
+            fv4u n1 = c >= 1 ? in4[c - 1] : z;
+            fv4u n2 = c >= 2 ? in4[c - 2] : z;
+            for (; c >= 0; c--) {
+                const fv4u w = cur;
+                cur = n1;
+                n1 = n2;
+                if (c >= 3) n2 = in4[c - 3];
+                uint4 e[16];  // table entries depend only on the symbols: read them all first
+#pragma unroll
+                for (int k = 15; k >= 0; k--) e[k] = s_e[(w[k >> 2] >> (8 * (k & 3))) & 0xFF];
+#pragma unroll
+                for (int k = 15; k >= 0; k--) step_e(e[k]);
+                if (err) break;
+            }
+        } else {
+            for (uint64_t i = full; i-- > 0;) step(in[i]);
         }
-        const uint64_t q = mul_hi_portable(x, s_rcp[sym]) >> s_shift[sym];
-        x = x + (uint64_t)s_bias[sym] + q * (uint64_t)s_cmpl[sym];
     }
     {
         const uint32_t qs[4] = {q0, q1, q2, q3};
@@ -603,85 +604,231 @@ __global__ __launch_bounds__(256) void k_fse_outscan(FseDecArgs a) {
 }
 
 // decode loop of decompress_single (fse.rs:1258-1278): decode_symbol
-// (fse.rs:664-676) then renormalize_decode (fse.rs:704-735). One lane per block.
-__global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
-    __shared__ uint8_t s_alias[4096];
-    __shared__ uint32_t s_fs[256];  // freq | start << 16
-    const uint64_t j = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-    const uint64_t nb = *a.nblocks;
-    const bool ok = *a.status == ZR_OK;
-    // table 0 into LDS when any block uses it
-    const FseDTab *T0 = &a.tabs[0];
-    const bool t0 = ok && nb > 0 && a.blk[0].raw == 0 && a.blk[0].orig > 0;
-    if (t0) {
-        for (int i = threadIdx.x; i < 1024; i += 64)
-            reinterpret_cast<uint32_t *>(s_alias)[i] = reinterpret_cast<const uint32_t *>(T0->alias)[i];
-        for (int i = threadIdx.x; i < 256; i += 64) s_fs[i] = T0->freq[i] | (T0->start[i] << 16);
+// (fse.rs:664-676) then renormalize_decode (fse.rs:704-735), one lane per
+// block. One LDS slot read per symbol; the word area is read backwards as
+// aligned 16-byte chunks (three chunks prefetched) and the 32-bit words are
+// funnel-shifted out of them (their misalignment is fixed for the block).
+template <bool SHARED>
+__device__ __forceinline__ void fse_dec_lane(const uint32_t *slot, const uint8_t *in, const uint8_t *wd, uint64_t bp,
+                                             uint64_t x, uint8_t *out, uint64_t orig) {
+    const fv4u z = {0, 0, 0, 0};
+    const uintptr_t wbase = (uintptr_t)wd;
+    const uintptr_t cmin = wbase >> 4;  // lowest chunk of the word area
+    // chunks are addressed from the (16-aligned-down) stream pointer so the
+    // loads stay in the global address space (no flat loads)
+    const fv4u *in4 = reinterpret_cast<const fv4u *>(in - (((uintptr_t)in) & 15));
+    const uintptr_t c0 = ((uintptr_t)in4) >> 4;
+    auto ld = [&](uintptr_t c) -> fv4u { return c >= cmin ? in4[c - c0] : z; };
+    uint32_t r8 = 0;
+    uintptr_t m = 0;  // absolute dword index of the next word's low dword
+    fv4u hi = z, cur = z, n1 = z, n2 = z, n3 = z;
+    if (bp >= 4) {
+        const uintptr_t a0 = wbase + bp - 4;
+        r8 = (uint32_t)(a0 & 3) * 8;
+        m = a0 >> 2;
+        const uintptr_t c = m >> 2;
+        // the chunk above is only needed when the first word's low dword is
+        // the last of its chunk; it then starts at or below the state bytes
+        if ((m & 3) == 3) hi = in4[c + 1 - c0];
+        cur = ld(c);
+        n1 = ld(c - 1);
+        n2 = ld(c - 2);
+        n3 = ld(c - 3);
     }
-    __syncthreads();
-    if (!ok || j >= nb) return;
-    const FseBlk B = a.blk[j];
-    uint8_t *out = a.out + a.ooff[j];
-    if (B.raw == 2 || B.orig == 0) return;
-    if (B.raw == 1) {
-        const uint8_t *src = a.in + B.body + 5;
-        for (uint64_t i = 0; i < B.orig; i++) out[i] = src[i];
-        return;
-    }
-    const bool shared = B.table == 0;
-    const FseDTab *T = &a.tabs[B.table];
-    const uint8_t *wd = a.in + B.words;
-    uint64_t bp = B.wbytes;
-    uint64_t x = B.state;
-    const bool vec = ((((uintptr_t)out) & 15) == 0);
-    // 16-byte output queue: acc collects 4 symbols, w0..w2 the completed
-    // dwords of the current 16-byte group.
-    uint32_t w0 = 0, w1 = 0, w2 = 0, acc = 0;
-    for (uint64_t i = 0; i < B.orig; i++) {
-        const uint32_t lo = (uint32_t)(x & 4095);
-        uint32_t s, f, st;
-        if (shared) {
-            s = s_alias[lo];
-            const uint32_t fs = s_fs[s];
-            f = fs & 0xFFFF;
-            st = fs >> 16;
-        } else {
-            s = T->alias[lo];
-            f = T->freq[s];
-            st = T->start[s];
-        }
-        x = (uint64_t)f * (x >> 12) + lo - st;
-        if (vec) {
-            acc = (acc >> 8) | (s << 24);
-            if ((i & 15) == 15) {
-                *reinterpret_cast<uint4 *>(out + i - 15) = make_uint4(w0, w1, w2, acc);
-            } else if ((i & 3) == 3) {
-                w0 = w1;
-                w1 = w2;
-                w2 = acc;
-            }
-        } else {
-            out[i] = (uint8_t)s;
-        }
+    auto step = [&]() -> uint32_t {
+        const uint32_t e = slot[x & 4095];
+        x = (uint64_t)(((e >> 8) & 4095) + 1) * (x >> 12) + (e >> 20);
         if (x < 65536 && bp > 0) {
             if (bp >= 4) {
                 bp -= 4;
-                x = (x << 32) | rd32(wd + bp);
+                const uint32_t k = (uint32_t)(m & 3);
+                const uint32_t lo32 = k == 0 ? cur.x : k == 1 ? cur.y : k == 2 ? cur.z : cur.w;
+                const uint32_t hi32 = k == 0 ? cur.y : k == 1 ? cur.z : k == 2 ? cur.w : hi.x;
+                x = (x << 32) | (uint32_t)((((uint64_t)hi32 << 32) | lo32) >> r8);
+                m -= 1;
+                if (k == 0) {
+                    hi = cur;
+                    cur = n1;
+                    n1 = n2;
+                    n2 = n3;
+                    n3 = ld((m >> 2) - 3);
+                }
             } else {
                 bp -= 1;
                 x = (x << 8) | wd[bp];
             }
         }
         if (x < 1) x = 1;
+        return e & 0xFF;
+    };
+    uint64_t i = 0;
+    if ((((uintptr_t)out) & 15) == 0) {
+        const uint64_t groups = orig >> 4;
+        fv4u *o4 = reinterpret_cast<fv4u *>(out);
+        for (uint64_t g = 0; g < groups; g++) {
+            uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 16; k++) o[k >> 2] |= step() << (8 * (k & 3));
+            o4[g] = fv4u{o[0], o[1], o[2], o[3]};
+        }
+        i = groups << 4;
     }
-    const uint32_t rem = (uint32_t)(B.orig & 15);
-    if (vec && rem) {
-        // partial last group: c completed dwords in w(3-c)..w2, r bytes in acc's top
-        const uint64_t g = B.orig - rem;
-        const uint32_t c = rem >> 2, r = rem & 3;
-        const uint32_t ws[3] = {w0, w1, w2};
-        for (uint32_t k = 0; k < c; k++) *reinterpret_cast<uint32_t *>(out + g + 4 * k) = ws[3 - c + k];
-        for (uint32_t t = 0; t < r; t++) out[g + 4 * c + t] = (uint8_t)(acc >> (8 * (4 - r + t)));
+    for (; i < orig; i++) out[i] = (uint8_t)step();
+}
+
+__device__ __forceinline__ void fse_asm_load16(fv4u &dst, const fv4u *p) {
+    // issued behind the compiler's back: the group pipeline below waits for it
+    // with a counted vmcnt instead of the vmcnt(0) the compiler would emit
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+}
+
+// Fast path for blocks coded with block 0's table (every block of a stream
+// this library or the reference wrote from one histogram). Per lane: a
+// 64-dword LDS ring of the word area indexed by absolute dword index mod 64
+// ([dword][lane] layout: conflict-free), refilled once per 16-symbol group by
+// two wave-uniform 16-byte loads that land two groups later behind
+// `s_waitcnt vmcnt(2)`. The next renormalisation word is read from the ring
+// one renormalisation ahead, so a step's dependency chain is one LDS slot read
+// plus integer arithmetic.
+__global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
+    __shared__ uint32_t s_slot[4096];
+    __shared__ uint32_t s_ring[64 * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t j = (uint64_t)blockIdx.x * 64 + lane;
+    const uint64_t nb = *a.nblocks;
+    if (*a.status != ZR_OK) return;  // uniform: status is not written by this kernel
+    const FseDTab *T0 = &a.tabs[0];
+    const bool t0 = nb > 0 && a.blk[0].raw == 0 && a.blk[0].orig > 0;
+    if (t0) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(T0->slot);
+        for (int i = lane; i < 1024; i += 64) reinterpret_cast<uint4 *>(s_slot)[i] = src[i];
+    }
+    __syncthreads();
+    FseBlk B = {};
+    if (j < nb) B = a.blk[j];
+    const bool coded = j < nb && B.raw == 0 && B.orig > 0;
+    const bool fast = coded && B.table == 0;
+    uint8_t *out = a.out + (j < nb ? a.ooff[j] : 0);
+
+    const fv4u *in4 = reinterpret_cast<const fv4u *>(a.in - (((uintptr_t)a.in) & 15));
+    const uintptr_t c0 = ((uintptr_t)in4) >> 4;
+    const uintptr_t wbase = (uintptr_t)(a.in + B.words);
+    const uintptr_t cmin = wbase >> 4;
+    uint64_t x = fast ? B.state : 1, bp = fast ? B.wbytes : 0;
+    uint32_t *ring = s_ring + lane;
+    auto rd = [&](uintptr_t d) -> uint32_t { return ring[(d & 63) * 64]; };
+    auto land = [&](const fv4u v, uintptr_t c) {
+        ring[((4 * c + 0) & 63) * 64] = v.x;
+        ring[((4 * c + 1) & 63) * 64] = v.y;
+        ring[((4 * c + 2) & 63) * 64] = v.z;
+        ring[((4 * c + 3) & 63) * 64] = v.w;
+    };
+    const uint32_t r8 = (uint32_t)((wbase + bp) & 3) * 8;
+    uintptr_t m = (wbase + bp - 4) >> 2;  // dword index of the next word's low dword
+    const uintptr_t ctop = (wbase + bp + 3) >> 4;
+    uintptr_t fc = ctop;  // next chunk to fetch (downwards)
+    if (fast) {
+        // initial fill: 16 chunks (state bytes follow the words, so ctop is in bounds)
+        for (int i = 0; i < 16 && fc >= cmin; i++, fc--) land(in4[fc - c0], fc);
+    }
+    auto read_word = [&](uintptr_t mm) -> uint32_t {
+        return (uint32_t)((((uint64_t)rd(mm + 1) << 32) | rd(mm)) >> r8);
+    };
+    uint32_t nw = fast && bp >= 4 ? read_word(m) : 0u;
+    auto step = [&]() -> uint32_t {
+        const uint32_t e = s_slot[x & 4095];
+        x = (uint64_t)(((e >> 8) & 4095) + 1) * (x >> 12) + (e >> 20);
+        // the common 32-bit renormalisation, branchless: the next word is
+        // re-read from the ring every step (LDS bandwidth is idle here)
+        const bool small = x < 65536;
+        const bool w4 = small && bp >= 4;
+        const bool w1 = small && bp > 0 && bp < 4;
+        x = w4 ? ((x << 32) | nw) : x;
+        bp -= w4 ? 4 : 0;
+        m -= w4 ? 1 : 0;
+        nw = read_word(m);
+        if (w1) {  // the last 1..3 bytes of a stream
+            bp -= 1;
+            const uintptr_t ad = wbase + bp;
+            x = (x << 8) | ((rd(ad >> 2) >> ((ad & 3) * 8)) & 0xFF);
+        }
+        x |= (x == 0) ? 1u : 0u;  // x = max(x, 1)
+        return e & 0xFF;
+    };
+    const uint32_t G = fast ? (uint32_t)(B.orig >> 4) : 0u;
+    const bool vec = (((uintptr_t)out) & 15) == 0;
+    uint32_t Gmax = vec ? G : 0u;  // unaligned output: everything in the tail loop
+    const uint32_t Gl = Gmax;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) Gmax = max(Gmax, (uint32_t)__shfl_xor((int)Gmax, d, 64));
+    fv4u A0 = {0, 0, 0, 0}, A1 = A0, B0 = A0, B1 = A0;
+    uint32_t fa = 0, fb = 0;
+    uintptr_t ca = 0, cb = 0;
+    auto issue = [&](fv4u &R0, fv4u &R1, uint32_t &fl, uintptr_t &cc) {
+        const uintptr_t need = (m + 1) >> 2;  // highest chunk still read
+        const bool f0 = fast && fc >= cmin && fc + 16 > need;
+        const bool f1 = f0 && fc >= cmin + 1 && fc + 15 > need;
+        cc = fc;
+        fse_asm_load16(R0, f0 ? in4 + (fc - c0) : in4);
+        fse_asm_load16(R1, f1 ? in4 + (fc - 1 - c0) : in4);
+        fl = (f0 ? 1u : 0u) | (f1 ? 2u : 0u);
+        fc -= (f0 ? 1 : 0) + (f1 ? 1 : 0);
+    };
+    auto settle = [&](const fv4u R0, const fv4u R1, uint32_t &fl, uintptr_t cc) {
+        if (fl & 1) land(R0, cc);
+        if (fl & 2) land(R1, cc - 1);
+        fl = 0;
+    };
+    // explicit global address space: a flat store would also count in lgkmcnt
+    // and every LDS wait of the next steps would wait for it
+    typedef __attribute__((address_space(1))) fv4u gfv4u;
+    typedef __attribute__((address_space(1))) uint8_t gu8;
+    gfv4u *o4 = (gfv4u *)(out);
+    gu8 *ob = (gu8 *)(out);
+    auto group = [&](uint32_t g) {
+        if (g < Gl) {
+            uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 16; k++) o[k >> 2] |= step() << (8 * (k & 3));
+            o4[g] = fv4u{o[0], o[1], o[2], o[3]};
+        }
+    };
+    for (uint32_t g = 0; g < Gmax; g += 2) {
+        if (g >= 2) {
+            asm volatile("s_waitcnt vmcnt(2)" : "+v"(A0), "+v"(A1)::"memory");
+            settle(A0, A1, fa, ca);
+        }
+        group(g);
+        issue(A0, A1, fa, ca);
+        if (g + 1 < Gmax) {
+            if (g + 1 >= 2) {
+                asm volatile("s_waitcnt vmcnt(2)" : "+v"(B0), "+v"(B1)::"memory");
+                settle(B0, B1, fb, cb);
+            }
+            group(g + 1);
+            issue(B0, B1, fb, cb);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(A0), "+v"(A1), "+v"(B0), "+v"(B1)::"memory");
+    settle(A0, A1, fa, ca);
+    settle(B0, B1, fb, cb);
+    if (fast) {
+        // tail (and every symbol of an unaligned output), refilling per symbol as needed
+        for (uint64_t i = (uint64_t)Gl << 4; i < B.orig; i++) {
+            if ((i & 15) == 0) {
+                const uintptr_t need = (m + 1) >> 2;
+                while (fc >= cmin && fc + 16 > need) {
+                    land(in4[fc - c0], fc);
+                    fc--;
+                }
+            }
+            ob[i] = (uint8_t)step();
+        }
+    } else if (coded) {
+        fse_dec_lane<false>(a.tabs[B.table].slot, a.in, a.in + B.words, B.wbytes, B.state, out, B.orig);
+    } else if (j < nb && B.raw == 1) {
+        const uint8_t *src = a.in + B.body + 5;
+        for (uint64_t i = 0; i < B.orig; i++) out[i] = src[i];
     }
 }
 
