@@ -153,6 +153,72 @@ int32_t zr_fse_decompress_dev(const uint8_t *in, size_t n, uint8_t *out, size_t 
                               uint64_t max_blocks, uint64_t *out_len_dev, int32_t *status_dev,
                               void *workspace, size_t workspace_bytes, void *stream);
 
+/* ======================================================================
+ * Huffman order-0 -- src/entropy/huffman/{tree,encoder,decoder}.rs
+ * ====================================================================== */
+typedef struct {
+    int32_t kind;             /* 0 empty, 1 single leaf (code "0"), 2 tree */
+    int32_t n_symbols;
+    uint32_t max_code_length; /* HuffmanTree::max_code_length */
+    uint8_t code_len[256];    /* 0: symbol not in the tree (get_code == None) */
+    uint64_t code[256];       /* bit i = i-th emitted bit (LSB-first packing) */
+    int32_t n_nodes;          /* decoding tree, node 0 = root */
+    int16_t child[511][2];    /* -1 on leaves */
+    uint8_t sym[511];         /* leaf symbol (placeholder leaves: 0) */
+} zr_huff_tree;
+
+/* HuffmanTree::from_frequencies                          tree.rs:52-133 */
+int32_t zr_huff_tree_build(const uint32_t freq[256], zr_huff_tree *t);
+size_t zr_huff_encode_bound(const zr_huff_tree *t, size_t n);
+/* HuffmanEncoder::encode                                 encoder.rs:88-131 */
+int32_t zr_huff_encode(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8_t *out,
+                       size_t out_cap, size_t *out_len);
+/* HuffmanDecoder::decode (output_length = n)             decoder.rs:90-165 */
+int32_t zr_huff_decode(const zr_huff_tree *t, const uint8_t *in, size_t in_len, uint8_t *out,
+                       size_t n);
+/* device-resident; the tree is passed by host pointer (it is uploaded with
+ * the launch). Decoding synchronises the stream between its segment
+ * synchronisation rounds. */
+size_t zr_huff_workspace_bytes(size_t n, size_t in_len);
+int32_t zr_huff_encode_dev(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8_t *out,
+                           size_t out_cap, uint64_t *out_len_dev, int32_t *status_dev,
+                           void *workspace, size_t workspace_bytes, void *stream);
+int32_t zr_huff_decode_dev(const zr_huff_tree *t, const uint8_t *in, size_t in_len, uint8_t *out,
+                           size_t n, int32_t *status_dev, void *workspace,
+                           size_t workspace_bytes, void *stream);
+
+/* ======================================================================
+ * Contextual Huffman order-1/2 -- src/entropy/huffman/interleaved.rs
+ * Every order-1/2 context tree holds all 256 symbols (interleaved.rs:160-171),
+ * so each is the fixed 8-bit rank code (tree.rs:122-126) and the coded
+ * stream is the byte sequence itself (x1) or its N-way chunk round-robin
+ * (encode_xn, interleaved.rs:704-761). Order 2 trained on < 3 bytes is order 1
+ * (interleaved.rs:191-193); order 1 trained on < 2 bytes is order 0 over that
+ * data (interleaved.rs:119-121): zr_ctx_huff_order reports the effective order.
+ * ====================================================================== */
+typedef struct zr_ctx_huff zr_ctx_huff;
+/* ContextualHuffmanEncoder::new(data, order)             interleaved.rs:94-266 */
+int32_t zr_ctx_huff_new(const uint8_t *train, size_t n, int32_t order, zr_ctx_huff **out);
+void zr_ctx_huff_free(zr_ctx_huff *h);
+int32_t zr_ctx_huff_order(const zr_ctx_huff *h);        /* effective order */
+size_t zr_ctx_huff_encode_bound(const zr_ctx_huff *h, size_t n);
+/* encode (interleaved.rs:269-392); nway 0 = encode(), 1/2/4/8 =
+ * encode_with_interleaving(X1..X8) (order 1 only, interleaved.rs:604-626) */
+int32_t zr_ctx_huff_encode(const zr_ctx_huff *h, int32_t nway, const uint8_t *in, size_t n,
+                           uint8_t *out, size_t out_cap, size_t *out_len);
+/* ContextualHuffmanDecoder::decode (nway 0, interleaved.rs:1050-1209) or
+ * decode_with_interleaving (nway 1/2/4/8, interleaved.rs:628-647, :764-822) */
+int32_t zr_ctx_huff_decode(const zr_ctx_huff *h, int32_t nway, const uint8_t *in, size_t in_len,
+                           uint8_t *out, size_t n, size_t *out_len);
+/* device-resident order-1/2 coding (identity / N-way round-robin transpose);
+ * ZR_UNSUPPORTED for an order-0 model (use zr_huff_*_dev with its tree) */
+int32_t zr_ctx_huff_encode_dev(const zr_ctx_huff *h, int32_t nway, const uint8_t *in, size_t n,
+                               uint8_t *out, void *stream);
+int32_t zr_ctx_huff_decode_dev(const zr_ctx_huff *h, int32_t nway, const uint8_t *in,
+                               size_t in_len, uint8_t *out, size_t n, void *stream);
+/* the model's order-0 tree (trees[0]) */
+int32_t zr_ctx_huff_tree0(const zr_ctx_huff *h, zr_huff_tree *t);
+
 /* ---- device memory helpers (for hosts without a HIP binding) ---- */
 int32_t zr_malloc_dev(void **ptr, size_t bytes);
 int32_t zr_free_dev(void *ptr);

@@ -64,3 +64,12 @@ def test_golden_gpu_fse(zr):
         assert zr.fse_compress_with_config(d, cfg).hex() == c["compressed"]
         if not (c["config"].get("parallel_blocks") == 1 and len(d) > 2 * c["config"]["block_size"]):
             assert zr.fse_decompress(bytes.fromhex(c["compressed"])) == d
+
+
+@pytest.mark.gpu
+def test_golden_gpu_huffman(zr):
+    for c in load("huffman_o0"):
+        d = make_input(c["input"])
+        e = zr.HuffmanEncoder(d)
+        assert e.encode(d).hex() == c["encoded"]
+        assert zr.HuffmanDecoder(e.tree()).decode(bytes.fromhex(c["encoded"]), len(d)) == d

@@ -41,6 +41,13 @@ class FseConfig(ctypes.Structure):
                 ("block_size", ctypes.c_uint64), ("adaptive", ctypes.c_int32)]
 
 
+class HuffTree(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("n_symbols", ctypes.c_int32),
+                ("max_code_length", ctypes.c_uint32), ("code_len", ctypes.c_uint8 * 256),
+                ("code", ctypes.c_uint64 * 256), ("n_nodes", ctypes.c_int32),
+                ("child", (ctypes.c_int16 * 2) * 511), ("sym", ctypes.c_uint8 * 511)]
+
+
 # (name, restype, argtypes) for every exported symbol; tests check this list
 # against include/zipora_amd.h.
 SIGNATURES = [
@@ -79,6 +86,27 @@ SIGNATURES = [
     ("zr_fse_decode_workspace_bytes", c_sz, [ctypes.c_uint64]),
     ("zr_fse_decompress_dev", ctypes.c_int32, [c_vp, c_sz, c_vp, c_sz, ctypes.c_uint64, c_vp, c_vp,
                                                c_vp, c_sz, c_vp]),
+    ("zr_huff_tree_build", ctypes.c_int32, [c_u32p, ctypes.POINTER(HuffTree)]),
+    ("zr_huff_encode_bound", c_sz, [ctypes.POINTER(HuffTree), c_sz]),
+    ("zr_huff_encode", ctypes.c_int32, [ctypes.POINTER(HuffTree), c_u8p, c_sz, c_u8p, c_sz,
+                                        ctypes.POINTER(c_sz)]),
+    ("zr_huff_decode", ctypes.c_int32, [ctypes.POINTER(HuffTree), c_u8p, c_sz, c_u8p, c_sz]),
+    ("zr_huff_workspace_bytes", c_sz, [c_sz, c_sz]),
+    ("zr_huff_encode_dev", ctypes.c_int32, [ctypes.POINTER(HuffTree), c_vp, c_sz, c_vp, c_sz, c_vp,
+                                            c_vp, c_vp, c_sz, c_vp]),
+    ("zr_huff_decode_dev", ctypes.c_int32, [ctypes.POINTER(HuffTree), c_vp, c_sz, c_vp, c_sz, c_vp,
+                                            c_vp, c_sz, c_vp]),
+    ("zr_ctx_huff_new", ctypes.c_int32, [c_u8p, c_sz, ctypes.c_int32, ctypes.POINTER(c_vp)]),
+    ("zr_ctx_huff_free", None, [c_vp]),
+    ("zr_ctx_huff_order", ctypes.c_int32, [c_vp]),
+    ("zr_ctx_huff_encode_bound", c_sz, [c_vp, c_sz]),
+    ("zr_ctx_huff_encode", ctypes.c_int32, [c_vp, ctypes.c_int32, c_u8p, c_sz, c_u8p, c_sz,
+                                            ctypes.POINTER(c_sz)]),
+    ("zr_ctx_huff_decode", ctypes.c_int32, [c_vp, ctypes.c_int32, c_u8p, c_sz, c_u8p, c_sz,
+                                            ctypes.POINTER(c_sz)]),
+    ("zr_ctx_huff_encode_dev", ctypes.c_int32, [c_vp, ctypes.c_int32, c_vp, c_sz, c_vp, c_vp]),
+    ("zr_ctx_huff_decode_dev", ctypes.c_int32, [c_vp, ctypes.c_int32, c_vp, c_sz, c_vp, c_sz, c_vp]),
+    ("zr_ctx_huff_tree0", ctypes.c_int32, [c_vp, ctypes.POINTER(HuffTree)]),
     ("zr_malloc_dev", ctypes.c_int32, [ctypes.POINTER(c_vp), c_sz]),
     ("zr_free_dev", ctypes.c_int32, [c_vp]),
     ("zr_memcpy_h2d", ctypes.c_int32, [c_vp, c_vp, c_sz, c_vp]),

@@ -1,0 +1,920 @@
+// zr_huff.hip -- Huffman order-0 (src/entropy/huffman/{tree,encoder,decoder}.rs)
+// and contextual order-1/2 (interleaved.rs) on MI355X / gfx950.
+//
+// Tree construction (H1) is host code: <= 256 leaves, a Rust BinaryHeap
+// emulation. The coding is on the GPU:
+//   encode (H2): code-length reduction -> block scan -> bit scatter with
+//     atomicOr into a word image -> byte copy-out;
+//   decode (H3): the stream is cut into fixed bit segments; every segment is
+//     decoded from a guessed code boundary and the guesses are repaired by
+//     propagating each segment's end into the next one until no start moves
+//     (Huffman codes self-synchronise within a few codes); then a count scan
+//     and a final decode pass that writes the symbols. Tables are 8-bit
+//     multi-level LUTs built on the host from the decoding tree.
+//   order 1/2 (H4-H6): every context tree holds all 256 symbols, so codes are
+//     the fixed 8-bit rank codes == the byte itself; encode/decode are a
+//     vectorised copy (x1) or the N-way chunk round-robin transpose.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "zr_internal.h"
+
+namespace zr {
+
+// ------------------------------------------------------------------ H1 (host)
+namespace {
+struct BNode {
+    uint32_t freq;
+    int32_t sym;  // -1 internal
+    int32_t l, r;
+};
+
+// std::collections::BinaryHeap (max-heap over `Reverse(node)`; the node order
+// of tree.rs:29-40 makes the element with the HIGHEST frequency the max).
+struct RustHeap {
+    std::vector<int32_t> d;
+    const std::vector<BNode> *nodes;
+    bool le(int32_t a, int32_t b) const { return (*nodes)[a].freq <= (*nodes)[b].freq; }
+    size_t sift_up(size_t start, size_t pos) {
+        const int32_t e = d[pos];
+        while (pos > start) {
+            const size_t parent = (pos - 1) / 2;
+            if (le(e, d[parent])) break;
+            d[pos] = d[parent];
+            pos = parent;
+        }
+        d[pos] = e;
+        return pos;
+    }
+    void push(int32_t x) {
+        d.push_back(x);
+        sift_up(0, d.size() - 1);
+    }
+    void sift_down_to_bottom(size_t pos) {
+        const size_t end = d.size(), start = pos;
+        const int32_t e = d[pos];
+        size_t child = 2 * pos + 1;
+        while (end >= 2 && child <= end - 2) {
+            if (le(d[child], d[child + 1])) child += 1;
+            d[pos] = d[child];
+            pos = child;
+            child = 2 * pos + 1;
+        }
+        if (child == end - 1) {
+            d[pos] = d[child];
+            pos = child;
+        }
+        d[pos] = e;
+        sift_up(start, pos);
+    }
+    int32_t pop() {
+        int32_t item = d.back();
+        d.pop_back();
+        if (!d.empty()) {
+            std::swap(item, d[0]);
+            sift_down_to_bottom(0);
+        }
+        return item;
+    }
+};
+
+int new_node(zr_huff_tree *t, int sym) {
+    const int i = t->n_nodes++;
+    t->child[i][0] = t->child[i][1] = -1;
+    t->sym[i] = (uint8_t)(sym < 0 ? 0 : sym);
+    return i;
+}
+
+// from_frequencies_fixed_length (tree.rs:136-175) + build_decoding_tree_from_codes
+// (tree.rs:311-350) + insert_code_into_tree (tree.rs:359-469).
+int32_t fixed_tree(const uint32_t freq[256], zr_huff_tree *t) {
+    memset(t->code_len, 0, sizeof(t->code_len));
+    memset(t->code, 0, sizeof(t->code));
+    t->n_nodes = 0;
+    int rank = 0;
+    for (int s = 0; s < 256; s++)
+        if (freq[s]) {
+            t->code_len[s] = 8;
+            t->code[s] = (uint64_t)rank++;  // rank bits, LSB first
+        }
+    t->n_symbols = rank;
+    t->max_code_length = 8;
+    t->kind = 2;
+    // the decoding tree of a complete set of distinct 8-bit codes: internal
+    // nodes down to depth 8, leaves carry their code's symbol; codes that no
+    // symbol owns end in placeholder leaves (symbol 0)
+    std::vector<int> placeholder;
+    auto mk = [&](int sym, bool ph) {
+        const int i = new_node(t, sym);
+        placeholder.resize(t->n_nodes);
+        placeholder[i] = ph ? 1 : 0;
+        return i;
+    };
+    const int root = mk(0, false);
+    t->child[root][0] = (int16_t)mk(0, true);
+    t->child[root][1] = (int16_t)mk(0, true);
+    for (int s = 0; s < 256; s++) {
+        if (!t->code_len[s]) continue;
+        int node = root;
+        for (int b = 0; b < 8; b++) {
+            const int bit = (int)((t->code[s] >> b) & 1);
+            int c = t->child[node][bit];
+            if (b == 7) {
+                if (!placeholder[c]) return set_error(ZR_INVALID_INPUT, "Code collision");
+                placeholder[c] = 0;
+                t->sym[c] = (uint8_t)s;
+                break;
+            }
+            if (t->child[c][0] < 0) {  // leaf: placeholder -> internal with two placeholders
+                if (!placeholder[c]) return set_error(ZR_INVALID_INPUT, "Code collision");
+                placeholder[c] = 0;
+                const int a = mk(0, true), z = mk(0, true);
+                t->child[c][0] = (int16_t)a;
+                t->child[c][1] = (int16_t)z;
+            }
+            node = c;
+        }
+    }
+    return ZR_OK;
+}
+}  // namespace
+
+int32_t huff_build(const uint32_t freq[256], zr_huff_tree *t) {
+    memset(t, 0, sizeof(*t));
+    std::vector<BNode> nodes;
+    nodes.reserve(512);
+    RustHeap h;
+    h.nodes = &nodes;
+    for (int s = 0; s < 256; s++)
+        if (freq[s]) {  // leaves pushed in byte order (tree.rs:59-67)
+            nodes.push_back({freq[s], s, -1, -1});
+            h.push((int32_t)nodes.size() - 1);
+        }
+    const int count = (int)nodes.size();
+    t->n_symbols = count;
+    if (count == 0) {  // tree.rs:69-75
+        t->kind = 0;
+        return ZR_OK;
+    }
+    if (count == 1) {  // tree.rs:78-90: the code is [false]
+        const int s = nodes[h.pop()].sym;
+        t->kind = 1;
+        t->code_len[s] = 1;
+        t->code[s] = 0;
+        t->max_code_length = 1;
+        new_node(t, s);
+        return ZR_OK;
+    }
+    while (h.d.size() > 1) {  // tree.rs:93-111
+        const int32_t l = h.pop(), r = h.pop();
+        nodes.push_back({nodes[l].freq + nodes[r].freq, -1, l, r});  // u32 add wraps (release)
+        h.push((int32_t)nodes.size() - 1);
+    }
+    const int32_t root = h.pop();
+    // generate_codes (tree.rs:187-208): left = 0, right = 1; depth-first with
+    // an explicit stack (a chain tree is up to 255 deep)
+    uint32_t maxlen = 0;
+    struct Fr {
+        int32_t n;
+        uint32_t len;
+        uint64_t code;
+    };
+    std::vector<Fr> st;
+    st.push_back({root, 0, 0});
+    while (!st.empty()) {
+        const Fr f = st.back();
+        st.pop_back();
+        const BNode &b = nodes[f.n];
+        if (b.sym >= 0) {
+            maxlen = std::max(maxlen, f.len);
+            t->code_len[b.sym] = (uint8_t)std::min<uint32_t>(f.len, 255);
+            t->code[b.sym] = f.code;
+            continue;
+        }
+        st.push_back({b.r, f.len + 1, f.len < 64 ? (f.code | (1ull << f.len)) : f.code});
+        st.push_back({b.l, f.len + 1, f.code});
+    }
+    if (maxlen > 64) return fixed_tree(freq, t);  // tree.rs:122-126
+    t->kind = 2;
+    t->max_code_length = maxlen;
+    // decoding tree = the build tree, preorder numbered from the root
+    std::vector<std::pair<int32_t, int32_t>> work;  // (build node, parent slot)
+    work.push_back({root, -1});
+    while (!work.empty()) {
+        const auto w = work.back();
+        work.pop_back();
+        const BNode &b = nodes[w.first];
+        const int me = new_node(t, b.sym);
+        if (w.second >= 0) t->child[w.second >> 1][w.second & 1] = (int16_t)me;
+        if (b.sym < 0) {
+            work.push_back({b.r, me * 2 + 1});
+            work.push_back({b.l, me * 2 + 0});
+        }
+    }
+    return ZR_OK;
+}
+
+// multi-level 8-bit decode LUT: table k has 256 entries for the node it
+// starts at; entry = leaf: 1<<31 | bits << 8 | sym ; else next table index
+// (8 bits consumed).
+static void huff_lut(const zr_huff_tree *t, std::vector<uint32_t> &lut) {
+    lut.clear();
+    std::vector<int> tab_node{0}, node_tab(t->n_nodes, -1);
+    node_tab[0] = 0;
+    for (size_t k = 0; k < tab_node.size(); k++) {
+        const int start = tab_node[k];
+        lut.resize((k + 1) * 256);
+        for (uint32_t v = 0; v < 256; v++) {
+            int cur = start;
+            uint32_t used = 0, e = 0;
+            bool leaf = false;
+            while (used < 8) {
+                cur = t->child[cur][(v >> used) & 1];
+                used++;
+                if (t->child[cur][0] < 0) {
+                    leaf = true;
+                    break;
+                }
+            }
+            if (leaf) {
+                e = 0x80000000u | (used << 8) | t->sym[cur];
+            } else {
+                if (node_tab[cur] < 0) {
+                    node_tab[cur] = (int)tab_node.size();
+                    tab_node.push_back(cur);
+                }
+                e = (uint32_t)node_tab[cur];
+            }
+            lut[k * 256 + v] = e;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ H2 (GPU)
+constexpr uint32_t HE_SYM = 16;                 // symbols per thread
+constexpr uint32_t HE_BLK = 256 * HE_SYM;       // symbols per workgroup
+
+struct HuffCodes {
+    uint64_t code[256];
+    uint32_t len[256];
+};
+
+__device__ __forceinline__ uint64_t blk_excl_scan_u64(uint64_t v, unsigned long long *sh, uint64_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        unsigned long long t = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += t;
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    unsigned long long base = 0;
+    for (int i = 0; i < w; i++) base += sh[i];
+    if (total) *total = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+    return base + inc - v;
+}
+
+// the code table travels as a by-value kernel argument (3 KiB of kernarg)
+__global__ __launch_bounds__(256) void k_huff_enc_len(const uint8_t *in, uint64_t n, const HuffCodes hc,
+                                                      uint64_t *blocksum, int32_t *status) {
+    __shared__ uint32_t s_len[256];
+    __shared__ unsigned long long sh[4];
+    s_len[threadIdx.x] = hc.len[threadIdx.x];
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * HE_BLK + (uint64_t)threadIdx.x * HE_SYM;
+    uint64_t bits = 0;
+    bool miss = false;
+    for (uint32_t k = 0; k < HE_SYM; k++) {
+        const uint64_t i = base + k;
+        if (i < n) {
+            const uint32_t L = s_len[in[i]];
+            miss |= L == 0;
+            bits += L;
+        }
+    }
+    if (miss) *status = ZR_INVALID_INPUT;  // "Symbol {} not in Huffman tree" (encoder.rs:96-101)
+    uint64_t tot;
+    blk_excl_scan_u64(bits, sh, &tot);
+    if (threadIdx.x == 0) blocksum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_huff_scan(uint64_t *v, uint64_t nb, uint64_t *total_bits,
+                                                   uint64_t *out_len, const int32_t *status) {
+    __shared__ unsigned long long sh[4];
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nb; base += 256) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t x = i < nb ? v[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = blk_excl_scan_u64(x, sh, &tot);
+        if (i < nb) v[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        if (total_bits) *total_bits = carry;
+        if (out_len) *out_len = (status && *status) ? 0 : (carry + 7) / 8;
+    }
+}
+
+__device__ __forceinline__ void put_bits32(uint32_t *W, uint64_t p, uint32_t v, uint32_t L) {
+    // v holds L <= 32 bits; OR them in at bit position p (LSB-first)
+    if (L == 0) return;
+    const uint64_t w = p >> 5;
+    const uint32_t sh = (uint32_t)(p & 31);
+    atomicOr(&W[w], v << sh);
+    if (sh + L > 32) atomicOr(&W[w + 1], v >> (32 - sh));
+}
+
+__global__ __launch_bounds__(256) void k_huff_enc_write(const uint8_t *in, uint64_t n, const HuffCodes hc,
+                                                        const uint64_t *blockoff, uint32_t *W,
+                                                        const int32_t *status) {
+    __shared__ uint32_t s_len[256];
+    __shared__ uint64_t s_code[256];
+    __shared__ unsigned long long sh[4];
+    s_len[threadIdx.x] = hc.len[threadIdx.x];
+    s_code[threadIdx.x] = hc.code[threadIdx.x];
+    __syncthreads();
+    if (*status) return;  // uniform: written only by the previous kernel
+    const uint64_t base = (uint64_t)blockIdx.x * HE_BLK + (uint64_t)threadIdx.x * HE_SYM;
+    uint8_t syms[HE_SYM];
+    uint64_t bits = 0;
+    for (uint32_t k = 0; k < HE_SYM; k++) {
+        const uint64_t i = base + k;
+        syms[k] = i < n ? in[i] : 0;
+        bits += i < n ? s_len[syms[k]] : 0;
+    }
+    uint64_t p = blockoff[blockIdx.x] + blk_excl_scan_u64(bits, sh, nullptr);
+    // gather into a 64-bit accumulator; emit whole 32-bit words
+    uint64_t acc = 0;
+    uint32_t na = 0;
+    const uint32_t lead = (uint32_t)(p & 31);  // first partial word is shared with the left neighbour
+    uint64_t wp = p - lead;                     // bit position of acc's bit 0
+    acc = 0;
+    na = lead;
+    for (uint32_t k = 0; k < HE_SYM; k++) {
+        if (base + k >= n) break;
+        const uint32_t L = s_len[syms[k]];
+        const uint64_t c = s_code[syms[k]];
+        uint32_t done = 0;
+        while (done < L) {
+            const uint32_t take = min(L - done, 32u);
+            const uint64_t part = (c >> done) & ((take == 32) ? 0xFFFFFFFFull : ((1ull << take) - 1));
+            acc |= part << na;
+            na += take;
+            done += take;
+            if (na >= 32) {
+                atomicOr(&W[wp >> 5], (uint32_t)acc);
+                acc >>= 32;
+                na -= 32;
+                wp += 32;
+            }
+        }
+    }
+    if (na > 0) atomicOr(&W[wp >> 5], (uint32_t)acc);
+}
+
+__global__ void k_copy_bytes(const uint8_t *src, uint8_t *dst, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+__global__ void k_copy_dev_len(const uint8_t *src, uint8_t *dst, const uint64_t *len, const int32_t *status) {
+    if (*status) return;
+    const uint64_t n = *len;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+// ------------------------------------------------------------------ H3 (GPU)
+constexpr uint64_t HD_SEG = 4096;  // bits per segment (>= the 64-bit longest code)
+
+struct HuffDecArgs {
+    const uint32_t *W;  // stream as little-endian words (+ two zero words of padding)
+    uint64_t B;         // stream bits
+    uint64_t nseg;
+    const uint32_t *lut;
+    uint64_t *start, *end;
+    uint64_t *cnt;      // codes per segment, then their exclusive scan
+    uint8_t *dirty;
+    uint32_t *changed;
+    uint8_t *out;
+    uint64_t n;
+};
+
+__device__ __forceinline__ uint32_t peek8(const uint32_t *W, uint64_t p) {
+    const uint64_t w = p >> 5;
+    const uint64_t v = ((uint64_t)W[w + 1] << 32) | W[w];
+    return (uint32_t)(v >> (p & 31)) & 0xFF;
+}
+
+// decode codes from p while p < lim; a code must complete within B.
+// Returns the number of codes; *pe = position after the last code (or B when
+// the stream ends inside a code).
+template <bool WRITE>
+__device__ uint64_t seg_decode(const HuffDecArgs &a, uint64_t p, uint64_t lim, uint64_t *pe, uint64_t obase) {
+    uint64_t c = 0;
+    while (p < lim) {
+        uint32_t tab = 0;
+        uint64_t q = p;
+        uint32_t e;
+        for (;;) {
+            e = a.lut[tab * 256 + peek8(a.W, q)];
+            if (e & 0x80000000u) {
+                q += (e >> 8) & 0xFF;
+                break;
+            }
+            q += 8;
+            tab = e;
+            if (q >= a.B) break;  // ran off the end inside a code
+        }
+        if (!(e & 0x80000000u) || q > a.B) {  // incomplete final code
+            *pe = a.B;
+            return c;
+        }
+        if (WRITE) {
+            const uint64_t o = obase + c;
+            if (o < a.n) a.out[o] = (uint8_t)e;
+        }
+        c++;
+        p = q;
+    }
+    *pe = p;
+    return c;
+}
+
+__global__ __launch_bounds__(256) void k_huff_seg(HuffDecArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.nseg || !a.dirty[t]) return;
+    const uint64_t lim = min((t + 1) * HD_SEG, a.B);
+    uint64_t pe;
+    a.cnt[t] = seg_decode<false>(a, a.start[t], lim, &pe, 0);
+    a.end[t] = pe;
+    a.dirty[t] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_huff_fix(HuffDecArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t == 0 || t >= a.nseg) return;
+    const uint64_t s = a.end[t - 1];
+    if (s != a.start[t]) {
+        a.start[t] = s;
+        a.dirty[t] = 1;
+        *a.changed = 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_huff_write(HuffDecArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.nseg) return;
+    const uint64_t o = a.cnt[t];
+    if (o >= a.n) return;
+    const uint64_t lim = min((t + 1) * HD_SEG, a.B);
+    uint64_t pe;
+    seg_decode<true>(a, a.start[t], lim, &pe, o);
+}
+
+__global__ void k_fill(uint8_t *out, uint64_t n, uint8_t v) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = v;
+}
+
+// ------------------------------------------------------------ H5/H6 (GPU)
+// x1: 16-byte vector copy. xN: out[i*N + k] = in[start_k + i] (the round
+// robin of encode_xn, interleaved.rs:704-761), inverse for decode.
+__global__ __launch_bounds__(256) void k_copy16(const uint8_t *src, uint8_t *dst, uint64_t n) {
+    const uint64_t nv = n >> 4;
+    typedef unsigned v4 __attribute__((ext_vector_type(4)));
+    const v4 *s4 = reinterpret_cast<const v4 *>(src);
+    v4 *d4 = reinterpret_cast<v4 *>(dst);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+        const v4 v = __builtin_nontemporal_load(&s4[i]);
+        __builtin_nontemporal_store(v, &d4[i]);
+    }
+    for (uint64_t i = (nv << 4) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        dst[i] = src[i];
+}
+
+template <int N, bool ENC>
+__global__ __launch_bounds__(256) void k_xn(const uint8_t *src, uint8_t *dst, uint64_t n) {
+    const uint64_t q = n / N, r = n % N;
+    const uint64_t rounds = q + (r ? 1 : 0);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rounds; i += stride) {
+        const uint32_t kk = i < q ? N : (uint32_t)r;
+        uint8_t v[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const uint64_t sk = (uint64_t)k * q + min((uint64_t)k, r);
+            if ((uint32_t)k < kk) {
+                if (ENC) v[k] = src[sk + i];
+                else dst[sk + i] = src[i * N + k];
+            }
+        }
+        if (ENC) {
+            if (kk == N && (((uintptr_t)(dst + i * N)) % N) == 0) {
+                if constexpr (N == 8) {
+                    uint2 w;
+                    w.x = v[0] | (v[1] << 8) | (v[2] << 16) | ((uint32_t)v[3] << 24);
+                    w.y = v[4] | (v[5] << 8) | (v[6] << 16) | ((uint32_t)v[7] << 24);
+                    *reinterpret_cast<uint2 *>(dst + i * N) = w;
+                } else if constexpr (N == 4) {
+                    *reinterpret_cast<uint32_t *>(dst + i * N) =
+                        v[0] | (v[1] << 8) | (v[2] << 16) | ((uint32_t)v[3] << 24);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < N; k++) dst[i * N + k] = v[k];
+                }
+            } else {
+                for (uint32_t k = 0; k < kk; k++) dst[i * N + k] = v[k];
+            }
+        }
+    }
+}
+
+static void launch_xn(int nway, bool enc, const uint8_t *src, uint8_t *dst, uint64_t n, hipStream_t s) {
+    const uint64_t per = (n + nway - 1) / nway;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(per, 256), 65535));
+#define ZR_XN(NW)                                                                      \
+    if (nway == NW) {                                                                 \
+        if (enc) hipLaunchKernelGGL((k_xn<NW, true>), dim3(grid), dim3(256), 0, s, src, dst, n); \
+        else hipLaunchKernelGGL((k_xn<NW, false>), dim3(grid), dim3(256), 0, s, src, dst, n);   \
+    }
+    ZR_XN(2) ZR_XN(4) ZR_XN(8)
+#undef ZR_XN
+}
+
+static void launch_copy(const uint8_t *src, uint8_t *dst, uint64_t n, hipStream_t s) {
+    if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0) {
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n >> 4, 256), 8192));
+        hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, s, src, dst, n);
+    } else {
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n, 256), 1u << 30));
+        hipLaunchKernelGGL(k_copy_bytes, dim3(grid), dim3(256), 0, s, src, dst, n);
+    }
+}
+
+}  // namespace zr
+
+using namespace zr;
+
+struct zr_ctx_huff {
+    int32_t order;     // effective order
+    zr_huff_tree t0;   // order 0: the model; order 1/2: trees[0] (all 256 symbols)
+};
+
+extern "C" {
+
+int32_t zr_huff_tree_build(const uint32_t freq[256], zr_huff_tree *t) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    return huff_build(freq, t);
+    ZR_GUARD_END
+}
+
+size_t zr_huff_encode_bound(const zr_huff_tree *t, size_t n) {
+    return (size_t)((n * (uint64_t)std::max<uint32_t>(t->max_code_length, 1) + 7) / 8) + 16;
+}
+
+size_t zr_huff_workspace_bytes(size_t n, size_t in_len) {
+    const uint64_t nb = ceil_div(std::max<size_t>(n, 1), HE_BLK);
+    const uint64_t enc = 4096 + round_up(sizeof(HuffCodes), 256) + round_up(8 * nb, 256) +
+                         round_up((n * 64 + 7) / 8 + 64, 256);
+    const uint64_t B = (uint64_t)in_len * 8;
+    const uint64_t nseg = std::max<uint64_t>(1, ceil_div(B, HD_SEG));
+    const uint64_t dec = 4096 + round_up(in_len + 64, 256) + 3 * round_up(8 * nseg, 256) + round_up(nseg, 256) +
+                         round_up(4ull * 256 * 256, 256);
+    return (size_t)std::max(enc, dec);
+}
+
+int32_t zr_huff_encode_dev(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                           uint64_t *out_len_dev, int32_t *status_dev, void *ws, size_t ws_bytes, void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    hipStream_t s = (hipStream_t)stream;
+    ZR_HIP(hipMemsetAsync(status_dev, 0, 4, s));
+    if (n == 0) {  // encoder.rs:89-91
+        ZR_HIP(hipMemsetAsync(out_len_dev, 0, 8, s));
+        return ZR_OK;
+    }
+    if (ws_bytes < zr_huff_workspace_bytes(n, 0)) return set_error(ZR_INVALID_INPUT, "workspace too small");
+    // the worst case: every symbol takes max_code_length bits
+    if (out_cap < zr_huff_encode_bound(t, n) - 16) return set_error(ZR_INVALID_INPUT, "output capacity too small");
+    uint8_t *w = reinterpret_cast<uint8_t *>(round_up((uintptr_t)ws, 256));
+    HuffCodes hc;
+    for (int i = 0; i < 256; i++) {
+        hc.code[i] = t->code[i];
+        hc.len[i] = t->code_len[i];
+    }
+    const uint64_t nb = ceil_div(n, HE_BLK);
+    uint64_t *bsum = reinterpret_cast<uint64_t *>(w);
+    w += round_up(8 * nb, 256);
+    uint32_t *W = reinterpret_cast<uint32_t *>(w);
+    const uint64_t maxbytes = (n * (uint64_t)std::max<uint32_t>(t->max_code_length, 1) + 7) / 8;
+    const uint64_t wbytes = round_up(maxbytes + 8, 4);
+    ZR_HIP(hipMemsetAsync(W, 0, wbytes, s));
+    timer_begin("huff_encode", s);
+    hipLaunchKernelGGL(k_huff_enc_len, dim3((uint32_t)nb), dim3(256), 0, s, in, (uint64_t)n, hc, bsum, status_dev);
+    hipLaunchKernelGGL(k_huff_scan, dim3(1), dim3(256), 0, s, bsum, nb, (uint64_t *)nullptr, out_len_dev,
+                       (const int32_t *)status_dev);
+    hipLaunchKernelGGL(k_huff_enc_write, dim3((uint32_t)nb), dim3(256), 0, s, in, (uint64_t)n, hc,
+                       (const uint64_t *)bsum, W, (const int32_t *)status_dev);
+    hipLaunchKernelGGL(k_copy_dev_len, dim3(1024), dim3(256), 0, s, (const uint8_t *)W, out,
+                       (const uint64_t *)out_len_dev, (const int32_t *)status_dev);
+    timer_end("huff_encode", s);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_huff_decode_dev(const zr_huff_tree *t, const uint8_t *in, size_t in_len, uint8_t *out, size_t n,
+                           int32_t *status_dev, void *ws, size_t ws_bytes, void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    hipStream_t s = (hipStream_t)stream;
+    ZR_HIP(hipMemsetAsync(status_dev, 0, 4, s));
+    if (in_len == 0 || n == 0) return ZR_OK;  // decoder.rs:91-93
+    if (t->kind == 0) return set_error(ZR_INVALID_INPUT, "Empty Huffman tree");
+    if (n / 64 > in_len || n > in_len * 64)  // decoder.rs:100-107
+        return set_error(ZR_INVALID_INPUT, "Implausible output length");
+    const uint64_t B = (uint64_t)in_len * 8;
+    if (t->kind == 1) {
+        // a single-leaf root emits one symbol per bit plus the final fix-up
+        // (decoder.rs:112-155): n symbols need n <= B + 1
+        if (n > B + 1) return set_error(ZR_INVALID_INPUT, "Decoded length mismatch");
+        hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, s, out, (uint64_t)n, t->sym[0]);
+        ZR_HIP(hipGetLastError());
+        return ZR_OK;
+    }
+    if (ws_bytes < zr_huff_workspace_bytes(0, in_len)) return set_error(ZR_INVALID_INPUT, "workspace too small");
+    std::vector<uint32_t> lut;
+    huff_lut(t, lut);
+    if (lut.size() > 256 * 256) return set_error(ZR_INTERNAL, "decode table too large");
+    uint8_t *w = reinterpret_cast<uint8_t *>(round_up((uintptr_t)ws, 256));
+    uint32_t *flag = reinterpret_cast<uint32_t *>(w);
+    w += 4096;
+    uint8_t *stream_copy = w;
+    w += round_up(in_len + 64, 256);
+    const uint64_t nseg = ceil_div(B, HD_SEG);
+    HuffDecArgs a;
+    a.W = reinterpret_cast<const uint32_t *>(stream_copy);
+    a.B = B;
+    a.nseg = nseg;
+    a.start = reinterpret_cast<uint64_t *>(w);
+    w += round_up(8 * nseg, 256);
+    a.end = reinterpret_cast<uint64_t *>(w);
+    w += round_up(8 * nseg, 256);
+    a.cnt = reinterpret_cast<uint64_t *>(w);
+    w += round_up(8 * nseg, 256);
+    a.dirty = w;
+    w += round_up(nseg, 256);
+    uint32_t *dlut = reinterpret_cast<uint32_t *>(w);
+    a.lut = dlut;
+    a.changed = flag;
+    a.out = out;
+    a.n = n;
+    ZR_HIP(hipMemsetAsync(stream_copy + in_len, 0, 64, s));
+    launch_copy(in, stream_copy, in_len, s);
+    ZR_HIP(hipMemcpyAsync(dlut, lut.data(), lut.size() * 4, hipMemcpyHostToDevice, s));
+    // segment starts: the guessed boundaries t * SEG
+    std::vector<uint64_t> st0(nseg);
+    for (uint64_t i = 0; i < nseg; i++) st0[i] = i * HD_SEG;
+    ZR_HIP(hipMemcpyAsync(a.start, st0.data(), 8 * nseg, hipMemcpyHostToDevice, s));
+    ZR_HIP(hipMemsetAsync(a.dirty, 1, nseg, s));
+    const uint32_t g = (uint32_t)ceil_div(nseg, 256);
+    timer_begin("huff_decode", s);
+    for (uint64_t it = 0; it <= nseg + 1; it++) {
+        hipLaunchKernelGGL(k_huff_seg, dim3(g), dim3(256), 0, s, a);
+        ZR_HIP(hipMemsetAsync(flag, 0, 4, s));
+        hipLaunchKernelGGL(k_huff_fix, dim3(g), dim3(256), 0, s, a);
+        uint32_t changed = 0;
+        ZR_HIP(hipMemcpyAsync(&changed, flag, 4, hipMemcpyDeviceToHost, s));
+        ZR_HIP(hipStreamSynchronize(s));
+        if (!changed) break;
+    }
+    uint64_t *tot = reinterpret_cast<uint64_t *>(flag + 2);
+    hipLaunchKernelGGL(k_huff_scan, dim3(1), dim3(256), 0, s, a.cnt, nseg, tot, (uint64_t *)nullptr,
+                       (const int32_t *)nullptr);
+    hipLaunchKernelGGL(k_huff_write, dim3(g), dim3(256), 0, s, a);
+    timer_end("huff_decode", s);
+    uint64_t total = 0;
+    ZR_HIP(hipMemcpyAsync(&total, tot, 8, hipMemcpyDeviceToHost, s));
+    ZR_HIP(hipStreamSynchronize(s));
+    if (total < n) {  // fewer complete codes than requested (decoder.rs:157-163)
+        const int32_t bad = ZR_INVALID_INPUT;
+        ZR_HIP(hipMemcpy(status_dev, &bad, 4, hipMemcpyHostToDevice));
+        return set_error(ZR_INVALID_INPUT, "Decoded length mismatch");
+    }
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+namespace {
+struct DMem {
+    void *p = nullptr;
+    ~DMem() {
+        if (p) (void)hipFree(p);
+    }
+};
+}  // namespace
+
+int32_t zr_huff_encode(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                       size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    *out_len = 0;
+    if (n == 0) return ZR_OK;
+    const size_t wsb = zr_huff_workspace_bytes(n, 0), cap = zr_huff_encode_bound(t, n);
+    DMem din, dout, dws, dm;
+    ZR_HIP(hipMalloc(&din.p, n));
+    ZR_HIP(hipMalloc(&dout.p, cap));
+    ZR_HIP(hipMalloc(&dws.p, wsb));
+    ZR_HIP(hipMalloc(&dm.p, 64));
+    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
+    uint64_t *olen = reinterpret_cast<uint64_t *>(dm.p);
+    int32_t *dst = reinterpret_cast<int32_t *>(olen + 1);
+    int32_t st = zr_huff_encode_dev(t, (const uint8_t *)din.p, n, (uint8_t *)dout.p, cap, olen, dst, dws.p, wsb,
+                                    nullptr);
+    if (st) return st;
+    ZR_HIP(hipDeviceSynchronize());
+    uint64_t meta[2];
+    ZR_HIP(hipMemcpy(meta, dm.p, 16, hipMemcpyDeviceToHost));
+    if ((int32_t)meta[1]) return set_error(ZR_INVALID_INPUT, "Symbol not in Huffman tree");
+    if (meta[0] > out_cap) return set_error(ZR_INVALID_INPUT, "output capacity too small");
+    ZR_HIP(hipMemcpy(out, dout.p, meta[0], hipMemcpyDeviceToHost));
+    *out_len = meta[0];
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_huff_decode(const zr_huff_tree *t, const uint8_t *in, size_t in_len, uint8_t *out, size_t n) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (in_len == 0 || n == 0) return ZR_OK;
+    const size_t wsb = zr_huff_workspace_bytes(0, in_len);
+    DMem din, dout, dws, dm;
+    ZR_HIP(hipMalloc(&din.p, in_len));
+    ZR_HIP(hipMalloc(&dout.p, n));
+    ZR_HIP(hipMalloc(&dws.p, wsb));
+    ZR_HIP(hipMalloc(&dm.p, 64));
+    ZR_HIP(hipMemcpy(din.p, in, in_len, hipMemcpyHostToDevice));
+    int32_t st = zr_huff_decode_dev(t, (const uint8_t *)din.p, in_len, (uint8_t *)dout.p, n, (int32_t *)dm.p,
+                                    dws.p, wsb, nullptr);
+    if (st) return st;
+    ZR_HIP(hipDeviceSynchronize());
+    ZR_HIP(hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+// ---------------------------------------------------------- contextual O1/O2
+int32_t zr_ctx_huff_new(const uint8_t *train, size_t n, int32_t order, zr_ctx_huff **out) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    *out = nullptr;
+    if (order < 0 || order > 2) return set_error(ZR_INVALID_INPUT, "order must be 0, 1 or 2");
+    int32_t eff = order;
+    if (eff == 2 && n < 3) eff = 1;  // interleaved.rs:191-193
+    if (eff == 1 && n < 2) eff = 0;  // interleaved.rs:119-121
+    zr_ctx_huff *h = new zr_ctx_huff();
+    h->order = eff;
+    uint32_t f[256] = {0};
+    if (eff == 0) {
+        // new_order0: HuffmanTree::from_data (tree.rs:178-184): the byte histogram
+        if (n) {
+            std::vector<uint32_t> hist(256, 0);
+            for (size_t i = 0; i < n; i++) hist[train[i]]++;
+            memcpy(f, hist.data(), sizeof(f));
+        }
+    } else {
+        // order-0 frequencies with zeros raised to 1 (interleaved.rs:131-136):
+        // all 256 symbols, so the tree is the fixed rank code (rank == byte)
+        for (int s = 0; s < 256; s++) f[s] = 1;
+    }
+    int32_t st = huff_build(f, &h->t0);
+    if (st) {
+        delete h;
+        return st;
+    }
+    *out = h;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+void zr_ctx_huff_free(zr_ctx_huff *h) { delete h; }
+int32_t zr_ctx_huff_order(const zr_ctx_huff *h) { return h->order; }
+
+int32_t zr_ctx_huff_tree0(const zr_ctx_huff *h, zr_huff_tree *t) {
+    *t = h->t0;
+    return ZR_OK;
+}
+
+size_t zr_ctx_huff_encode_bound(const zr_ctx_huff *h, size_t n) {
+    return h->order == 0 ? zr_huff_encode_bound(&h->t0, n) : n + 16;
+}
+
+int32_t zr_ctx_huff_encode_dev(const zr_ctx_huff *h, int32_t nway, const uint8_t *in, size_t n, uint8_t *out,
+                               void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (h->order == 0) return set_error(ZR_UNSUPPORTED, "order-0 model: use zr_huff_encode_dev");
+    if (nway != 0 && nway != 1 && nway != 2 && nway != 4 && nway != 8)
+        return set_error(ZR_INVALID_INPUT, "interleaving factor must be 1, 2, 4 or 8");
+    if (nway != 0 && h->order != 1)  // interleaved.rs:609-613
+        return set_error(ZR_INVALID_INPUT, "Interleaving only supported for Order-1 Huffman encoding");
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) return ZR_OK;
+    timer_begin("huff_o1_encode", s);
+    if (nway <= 1) launch_copy(in, out, n, s);
+    else launch_xn(nway, true, in, out, n, s);
+    timer_end("huff_o1_encode", s);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_ctx_huff_decode_dev(const zr_ctx_huff *h, int32_t nway, const uint8_t *in, size_t in_len,
+                               uint8_t *out, size_t n, void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (h->order == 0) return set_error(ZR_UNSUPPORTED, "order-0 model: use zr_huff_decode_dev");
+    if (nway != 0 && nway != 1 && nway != 2 && nway != 4 && nway != 8)
+        return set_error(ZR_INVALID_INPUT, "interleaving factor must be 1, 2, 4 or 8");
+    if (nway != 0 && h->order != 1)
+        return set_error(ZR_INVALID_INPUT, "Interleaving only supported for Order-1 Huffman decoding");
+    hipStream_t s = (hipStream_t)stream;
+    if (in_len == 0 || n == 0) return ZR_OK;
+    if (in_len < n) return set_error(ZR_INVALID_INPUT, "Unexpected end of stream");
+    timer_begin("huff_o1_decode", s);
+    if (nway <= 1) launch_copy(in, out, n, s);
+    else launch_xn(nway, false, in, out, n, s);
+    timer_end("huff_o1_decode", s);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_ctx_huff_encode(const zr_ctx_huff *h, int32_t nway, const uint8_t *in, size_t n, uint8_t *out,
+                           size_t out_cap, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    *out_len = 0;
+    if (h->order == 0) {
+        if (nway != 0) return set_error(ZR_INVALID_INPUT, "Interleaving only supported for Order-1 Huffman encoding");
+        return zr_huff_encode(&h->t0, in, n, out, out_cap, out_len);
+    }
+    if (nway != 0 && h->order != 1)
+        return set_error(ZR_INVALID_INPUT, "Interleaving only supported for Order-1 Huffman encoding");
+    if (n == 0) return ZR_OK;
+    if (out_cap < n) return set_error(ZR_INVALID_INPUT, "output capacity too small");
+    DMem din, dout;
+    ZR_HIP(hipMalloc(&din.p, n));
+    ZR_HIP(hipMalloc(&dout.p, n));
+    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
+    int32_t st = zr_ctx_huff_encode_dev(h, nway, (const uint8_t *)din.p, n, (uint8_t *)dout.p, nullptr);
+    if (st) return st;
+    ZR_HIP(hipDeviceSynchronize());
+    ZR_HIP(hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
+    *out_len = n;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_ctx_huff_decode(const zr_ctx_huff *h, int32_t nway, const uint8_t *in, size_t in_len, uint8_t *out,
+                           size_t n, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    *out_len = 0;
+    if (h->order == 0) {
+        if (nway != 0) return set_error(ZR_INVALID_INPUT, "Interleaving only supported for Order-1 Huffman decoding");
+        if (in_len == 0 || n == 0) return ZR_OK;
+        // decode_order0 (interleaved.rs:1082-1130) is the same walk as
+        // HuffmanDecoder::decode without the plausibility check, whose
+        // rejections the walk's length check also makes
+        if (h->t0.kind == 0) return set_error(ZR_INVALID_INPUT, "Empty Huffman tree");
+        if (n > (uint64_t)in_len * 8 + 1) return set_error(ZR_INVALID_INPUT, "Decoded length mismatch");
+        int32_t st = zr_huff_decode(&h->t0, in, in_len, out, n);
+        if (st == ZR_OK) *out_len = n;
+        return st;
+    }
+    if (nway != 0 && h->order != 1)
+        return set_error(ZR_INVALID_INPUT, "Interleaving only supported for Order-1 Huffman decoding");
+    if (in_len == 0 || n == 0) return ZR_OK;
+    if (in_len < n) return set_error(ZR_INVALID_INPUT, "Decoded length mismatch");
+    DMem din, dout;
+    ZR_HIP(hipMalloc(&din.p, in_len));
+    ZR_HIP(hipMalloc(&dout.p, n));
+    ZR_HIP(hipMemcpy(din.p, in, in_len, hipMemcpyHostToDevice));
+    int32_t st = zr_ctx_huff_decode_dev(h, nway, (const uint8_t *)din.p, in_len, (uint8_t *)dout.p, n, nullptr);
+    if (st) return st;
+    ZR_HIP(hipDeviceSynchronize());
+    ZR_HIP(hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
+    *out_len = n;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+}  // extern "C"
