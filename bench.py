@@ -76,6 +76,19 @@ def _table_fast(O, d):
     return O.rans_table([int(x) for x in h])
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per dispatch of `kernel` from the latest committed PMC summary
+    (profiles/<round>_traffic.json, made by tools/profile_round.sh +
+    tools/summarize_prof.py: FETCH_SIZE x2 + WRITE_SIZE, separate passes)."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not fs:
+        return None, None
+    with open(fs[-1]) as fh:
+        t = json.load(fh).get(kernel)
+    return (t["hbm_bytes"] if t else None), os.path.relpath(fs[-1], ROOT)
+
+
 def kernel_ms(L, name):
     ms, cnt = ctypes.c_double(0), ctypes.c_uint64(0)
     L.zr_timer_read(name.encode(), ctypes.byref(ms), ctypes.byref(cnt))
@@ -109,6 +122,7 @@ def cpu_baseline_fse(host, bs, threads):
 
 
 def run_fse(args, torch, dist, world, rank, dev, zr, L):
+    from zipora_amd import dist as zd
     """configs[2]: FSE encode+decode, 256 MiB Zipf(1.1) per GPU, 0xF6 blocks (Some(8))."""
     total = 256 << 20
     bs = args.fse_block_kib << 10
@@ -152,10 +166,7 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
     L.zr_timer_reset()
     if not torch.equal(out, raw):
         raise SystemExit("FSE decode mismatch in timed region")
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+    dt = zd.max_over_ranks(dt, dev)
     dec_bytes = clen + total
     achieved = dec_bytes / (dec_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
     res = {
@@ -168,7 +179,8 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
                                f"block_size={bs >> 10} KiB ({nblk} blocks, one coder lane each)",
                    "block_size": bs, "blocks": nblk, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_fse_dec",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_fse_dec")[0],
+                     "traffic_source": pmc_traffic("k_fse_dec")[1], "kernel": "k_fse_dec",
                      "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
         "kernels_ms": {"fse_decode": round(dec_ms, 4), "fse_encode": round(enc_ms, 4),
                        "fse_histogram": round(hist_ms, 4)},
@@ -193,6 +205,7 @@ def main():
     torch.cuda.set_device(dev)
 
     import zipora_amd as zr
+    from zipora_amd import dist as zd
     from zipora_amd.device import RansDeviceBatch
     L = zr.load()
     L.zr_set_device(local)
@@ -217,7 +230,7 @@ def main():
     def step():
         bt.histogram(raw, stream)
         if world > 1:  # the shared frequency table: RCCL all-reduce of 256 counts
-            dist.all_reduce(bt.hist, op=dist.ReduceOp.SUM)
+            zd.allreduce_histogram(bt.hist)
         bt.tables_from_hist(stream)
         bt.encode(raw, enc, stream)
         bt.decode(enc, out, stream)
@@ -260,10 +273,7 @@ def main():
             raise SystemExit("decode mismatch in timed region")
     comp_bytes = int(bt.enc_len.sum().item())
 
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+    dt = zd.max_over_ranks(dt, dev)
     value = world * total * args.steps / dt / 2**30
 
     # dominant kernel: the fast decode (reads C compressed bytes, writes N_in bytes)
@@ -288,8 +298,9 @@ def main():
                                f"shared table (histogram all-reduce over ranks)",
                    "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_dec_xn<false> (rans_decode)",
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic("k_dec_fast")[0], "traffic_source": pmc_traffic("k_dec_fast")[1],
+                     "kernel": "k_dec_fast (rans_decode)",
                      "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
         "kernels_ms": {"rans_decode": round(dec_ms, 4), "rans_encode": round(enc_ms, 4),
                        "rans_compact": round(cmp_ms, 4), "histogram": round(hist_ms, 4)},

@@ -1,0 +1,65 @@
+"""The N>1 path on CPU: world_size-2 gloo ranks run the shared-table exchange
+(histogram all-reduce) and the max-over-ranks timing of bench.py. Every rank
+must end with the same Rans64Encoder::new table, equal to the oracle's table
+for the union of the shards. (No GPU: the table build is host code.)"""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        import zipora_amd as zr
+        from zipora_amd import dist as zd
+        import oracle_ffi as O
+        shard = O.gen_uniform(50000 + 999 * rank, seed=zd.shard_seed(7, rank))[: 30000 + 5000 * rank]
+        h = torch.tensor(np.bincount(np.frombuffer(shard, dtype=np.uint8), minlength=256).astype(np.int64))
+        zd.allreduce_histogram(h)
+        enc = zr.Rans64Encoder([int(x) for x in h], 4096)
+        tab = [enc.get_symbol(s).freq for s in range(256)] + [enc.get_symbol(s).start for s in range(256)]
+        shards = [None] * world
+        dist.all_gather_object(shards, shard)
+        tabs = [None] * world
+        dist.all_gather_object(tabs, tab)
+        union = b"".join(shards)
+        ot = O.rans_table(O.histogram(union))
+        ref = list(ot.freq) + list(ot.start)
+        t = zd.max_over_ranks(0.5 + rank)
+        q.put((rank, all(x == ref for x in tabs), t))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shared_table_two_ranks():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res)
+    assert all(t == pytest.approx(1.5) for _, _, t in res)
