@@ -302,9 +302,13 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         x = valid ? xn : x;
     };
     uint32_t sc = 0;  // store instructions this wave issued since the last piece load
-    // full dwords queue in a 4-dword shift register; a lane stores 16 bytes at
-    // once (dwordx4), so each wave store instruction touches few lane addresses
-    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0;
+    // full dwords queue in a 4-dword shift register; every 16 bytes move to an
+    // LDS staging row ([chunk][lane], 1 KiB per wave store: conflict-free), and
+    // every 64 bytes a lane stores its 4 staged chunks back to back, so each
+    // 64-B segment of the scratch reaches the L2 in one burst (16-B stores
+    // spread over time were written back as partial lines: 2.4x the bytes).
+    __shared__ v4u stg[4 * 256];
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0, nstg = 0;
     v4u *out4 = reinterpret_cast<v4u *>(out);
     auto flush = [&]() {
         if (nacc >= 32) {
@@ -318,12 +322,26 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         }
         const bool need = nq == 4;
         if (__builtin_amdgcn_ballot_w64(need) != 0) {  // wave-uniform
-            sc++;
             if (need) {
-                if (ablate & 1) asm volatile("" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3));  // diagnostic
-                else out4[nout >> 2] = v4u{q0, q1, q2, q3};
-                nout += 4;
+                stg[(nstg & 3) * 256 + threadIdx.x] = v4u{q0, q1, q2, q3};
+                nstg++;
                 nq = 0;
+            }
+            const bool full = need && (nstg & 3) == 0;
+            if (__builtin_amdgcn_ballot_w64(full) != 0) {
+                sc += 4;
+                if (full) {
+                    const uint32_t o = nout >> 2;
+                    if (ablate & 1) {  // diagnostic
+                        asm volatile("" ::"v"(stg[threadIdx.x]));
+                    } else {
+                        out4[o + 0] = stg[0 * 256 + threadIdx.x];
+                        out4[o + 1] = stg[1 * 256 + threadIdx.x];
+                        out4[o + 2] = stg[2 * 256 + threadIdx.x];
+                        out4[o + 3] = stg[3 * 256 + threadIdx.x];
+                    }
+                    nout += 16;
+                }
             }
         }
     };
@@ -374,7 +392,9 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         }
     }
     wait_vmcnt_le(0, pend);
-    // drain: queued dwords (oldest in q[4-nq]) then the partial dword
+    // drain: staged chunks, queued dwords (oldest in q[4-nq]), the partial dword
+    for (uint32_t i = 0; i < (nstg & 3); i++) out4[(nout >> 2) + i] = stg[i * 256 + threadIdx.x];
+    nout += 4 * (nstg & 3);
     {
         const uint32_t qs[4] = {q0, q1, q2, q3};
         for (uint32_t i = 0; i < nq; i++) out[nout + i] = qs[4 - nq + i];
@@ -746,13 +766,16 @@ __global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw
 // ----------------------------------------------------------------------
 // Fast xN decode. One lane = one stream, FW = 512 lanes per workgroup share
 // one 16 KiB LDS slot table (2 workgroups per CU hold 1024 streams).
-//   * stream bytes: per-lane ring of RSLOTS x 16 B in LDS, layout [slot][lane].
+//   * stream bytes: per-lane ring of RSLOTS x 16 B in LDS, laid out
+//     [dword][lane] (bank = lane: conflict-free whatever each lane reads).
 //     Ring refills are wave-UNIFORM: every DTILE steps each lane writes the
 //     chunks it loaded DTILE steps earlier (register staged, so the global
 //     load latency overlaps a whole tile) and issues loads for up to two more.
 //     A lane only ever reads its own ring column, so no barrier is needed.
-//   * window: 64-bit MSB-first bit window refilled by one aligned dword per
-//     refill; the next dword is prefetched from the ring with the table read.
+//   * window: 64-bit MSB-first bit window. A step consumes at most 16 bits
+//     (x >= 16 after a decode), so one 32-bit refill per PAIR of steps keeps
+//     it >= 32 bits at every pair start; the next dword is prefetched from the
+//     ring one pair ahead.
 //   * output: 4 steps per lane are packed into a dword and 4x4-byte
 //     transposed across each lane quad with DPP, so every lane stores one
 //     aligned dword per 4 steps: row k+q, streams s0..s0+3.
@@ -775,13 +798,13 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
     if (n == 0 || single_mode(n, N) || a.status[b] != 0) return;
-    constexpr uint32_t RB = RSLOTS * 16;  // ring bytes per lane
+    constexpr uint32_t RD = RSLOTS * 4;  // ring dwords per lane
     __shared__ uint32_t stab[TOTFREQ];
-    __shared__ __attribute__((aligned(16))) uint8_t ringb[FW * RB];  // [lane][RB], chunk slots swizzled
+    __shared__ __attribute__((aligned(16))) uint32_t ringw[RD * FW];  // [dword][lane]
     // scan scratch and flag alias the ring (used before it is filled): keeps the
     // workgroup at exactly 80 KiB of LDS so two fit on a CU
-    unsigned long long *sh = reinterpret_cast<unsigned long long *>(ringb);
-    uint32_t *flag = reinterpret_cast<uint32_t *>(ringb) + 64;
+    unsigned long long *sh = reinterpret_cast<unsigned long long *>(ringw);
+    uint32_t *flag = ringw + 64;
     const uint32_t tid = threadIdx.x;
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
     for (uint32_t j = tid; j < TOTFREQ; j += FW) stab[j] = T->slot[j];
@@ -818,52 +841,71 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
     const uint64_t cmax = (n - 1) / N + 1;
     const uintptr_t sb = (uintptr_t)e + 12 * (size_t)N + off;  // stream start
     const uintptr_t lo_lim = ((uintptr_t)e) & ~(uintptr_t)15;     // safe lower bound for loads
-    const uint32_t lanebase = tid * RB;
-    const uint32_t lanex = (tid & (RSLOTS - 1)) << 4;  // slot swizzle: spreads equal offsets over banks
-    auto roff = [&](uint32_t addr) -> uint32_t { return lanebase + ((addr & (RB - 1)) ^ lanex); };
-    auto lds32 = [&](uint32_t o) -> uint32_t { return *reinterpret_cast<const uint32_t *>(ringb + o); };
+    uint32_t *ring = ringw + tid;
+    // byte address -> this lane's ring dword (the dword holding that address)
+    auto rdw = [&](uint32_t addr) -> uint32_t { return ring[((addr >> 2) & (RD - 1)) * FW]; };
+    auto put16 = [&](uint32_t addr, const v4u v) {  // chunk at 16-aligned addr
+        const uint32_t d = (addr >> 2) & (RD - 1);
+        ring[(d + 0) * FW] = v.x;
+        ring[(d + 1) * FW] = v.y;
+        ring[(d + 2) * FW] = v.z;
+        ring[(d + 3) * FW] = v.w;
+    };
     auto clampa = [&](uintptr_t addr) -> uintptr_t { return addr > lo_lim ? addr : lo_lim; };
-    // ---- ring prologue: the 4 chunks ending at the stream end, synchronously
+    // ---- ring prologue (synchronous): the 64-B segment holding the stream's
+    // last byte, and the segment below it. Later refills move whole 64-B
+    // segments (4 chunks issued back to back), so each L2 line is requested
+    // in one burst instead of chunk by chunk across tiles.
     const uintptr_t pend = sb + L;
-    uintptr_t lo = ((pend - 1) & ~(uintptr_t)15) + 16;  // lowest chunk loaded or in flight
+    const uintptr_t top = ((pend - 1) & ~(uintptr_t)15) + 16;  // end of the last chunk
+    uintptr_t lo = (top - 1) & ~(uintptr_t)63;                   // lowest byte loaded or in flight
     {
-        const v4u c0 = *reinterpret_cast<const v4u *>(clampa(lo - 16));
-        const v4u c1 = *reinterpret_cast<const v4u *>(clampa(lo - 32));
-        const v4u c2 = *reinterpret_cast<const v4u *>(clampa(lo - 48));
-        const v4u c3 = *reinterpret_cast<const v4u *>(clampa(lo - 64));
-        *reinterpret_cast<v4u *>(ringb + roff((uint32_t)(lo - 16))) = c0;
-        *reinterpret_cast<v4u *>(ringb + roff((uint32_t)(lo - 32))) = c1;
-        *reinterpret_cast<v4u *>(ringb + roff((uint32_t)(lo - 48))) = c2;
-        *reinterpret_cast<v4u *>(ringb + roff((uint32_t)(lo - 64))) = c3;
-        lo -= 64;
+        for (uintptr_t cpos = top - 16; cpos + 1 > lo; cpos -= 16)
+            put16((uint32_t)cpos, *reinterpret_cast<const v4u *>(clampa(cpos)));
+        const uintptr_t g = lo - 64;
+        const v4u c0 = *reinterpret_cast<const v4u *>(clampa(g + 48));
+        const v4u c1 = *reinterpret_cast<const v4u *>(clampa(g + 32));
+        const v4u c2 = *reinterpret_cast<const v4u *>(clampa(g + 16));
+        const v4u c3 = *reinterpret_cast<const v4u *>(clampa(g));
+        put16((uint32_t)(g + 48), c0);
+        put16((uint32_t)(g + 32), c1);
+        put16((uint32_t)(g + 16), c2);
+        put16((uint32_t)g, c3);
+        lo = g;
     }
     // window: the dword holding the last stream byte, its garbage top bytes shifted out
     const uintptr_t a0 = (pend - 1) & ~(uintptr_t)3;
     const uint32_t v0 = (uint32_t)(pend - a0);
     uint32_t x = (uint32_t)X;
-    uint64_t win = (uint64_t)(lds32(roff((uint32_t)a0)) << (32 - 8 * v0)) << 32;
+    uint64_t win = (uint64_t)(rdw((uint32_t)a0) << (32 - 8 * v0)) << 32;
     uint32_t nbits = 8 * v0;
     const uint32_t pend32 = (uint32_t)pend;
     uint32_t cons = (uint32_t)a0;  // (low 32 bits) bytes [cons, pend) have entered the window
-    uint32_t nextw = lds32(roff(cons - 4));
-    // staged chunks in flight. Inline asm so hipcc inserts no conservative
+    uint32_t nextw = rdw(cons - 4);
+    // a staged segment in flight. Inline asm so hipcc inserts no conservative
     // vmcnt(0) (it would also wait for the tile's stores); the boundary below
     // waits with an exact count instead.
-    v4u st0, st1;
-    asm_load16(st0, clampa(lo - 16));
-    asm_load16(st1, clampa(lo - 32));
-    uint32_t nst = 2;
-    uint32_t stlo = (uint32_t)(lo - 32);
-    lo -= 32;
+    v4u st0 = {0, 0, 0, 0}, st1 = st0, st2 = st0, st3 = st0;
+    bool pending = false;
+    uint32_t stlo = 0;
     // quad transpose selectors
     const uint32_t q = tid & 3;
     const uint32_t sel1 = q < 2 ? 0x05040100u : 0x03020706u;
     const uint32_t sel2 = (q & 1) ? 0x03070105u : 0x06020400u;
     const uint64_t s0 = s & ~3u;
-    uint32_t cons_snap = cons;
-    uint32_t nbits_snap = nbits;
     const bool wave_live = (uint64_t)blkF * FW + (tid & ~63u) < N;  // wave-uniform
 
+    // one 32-bit refill (branchless), then prefetch the next ring dword
+    auto refill = [&]() {
+        const bool need = nbits <= 32;
+        win |= (uint64_t)(need ? nextw : 0u) << ((32 - nbits) & 63);
+        nbits += need ? 32u : 0u;
+        cons -= need ? 4u : 0u;
+        nextw = rdw(cons - 4);
+    };
+    refill();  // >= 32 bits before the first pair
+    uint32_t cons_snap = cons;
+    uint32_t nbits_snap = nbits;
     // one decode step: renormalise (rans.rs:479-485) then decode (rans.rs:488-504)
     auto step = [&](const uint32_t selj, uint32_t &wd) {
         // x in [16, 2^24) needs 0, 1 or 2 bytes; the shift is 8 * #bytes
@@ -871,12 +913,6 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
         x = (uint32_t)(((((uint64_t)x) << 32) | (uint32_t)(win >> 32)) << sh8 >> 32);
         win <<= sh8;
         nbits -= sh8;
-        // branchless refill of one dword from the ring
-        const bool need = nbits <= 32;
-        win |= (uint64_t)(need ? nextw : 0u) << ((32 - nbits) & 63);
-        nbits += need ? 32u : 0u;
-        cons -= need ? 4u : 0u;
-        nextw = lds32(roff(cons - 4));
         const uint32_t ent = stab[x & (TOTFREQ - 1)];
         x = __umul24(ent >> 20, x >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
         wd = __builtin_amdgcn_perm(ent, wd, selj);
@@ -892,20 +928,29 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
     for (uint64_t k0 = 0; k0 < cmax; k0 += DTILE) {
         // ---- ring maintenance (wave-uniform position, per-lane masks)
         if (k0 > 0) {
-            // the previous boundary's chunk loads are followed by exactly 4 dword
+            // the previous boundary's segment loads are followed by exactly 4 dword
             // stores of this wave when that tile was full and the wave is live
-            if (prev_full && wave_live) asm volatile("s_waitcnt vmcnt(4)" : "+v"(st0), "+v"(st1)::"memory");
-            else asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1)::"memory");
-            if (nst >= 1) *reinterpret_cast<v4u *>(ringb + roff(stlo + 16 * (nst - 1))) = st0;
-            if (nst >= 2) *reinterpret_cast<v4u *>(ringb + roff(stlo)) = st1;
-            const uint32_t lo32 = (uint32_t)lo;
-            const uint32_t occ = ((cons - 1 - lo32) >> 4) + 1;
-            const uint32_t nl = min(2u, RSLOTS > occ ? RSLOTS - occ : 0u);
-            nst = nl;
-            if (nl >= 1) asm_load16(st0, clampa(lo - 16));
-            if (nl >= 2) asm_load16(st1, clampa(lo - 32));
-            lo -= 16 * nl;
-            stlo = (uint32_t)lo;
+            if (prev_full && wave_live)
+                asm volatile("s_waitcnt vmcnt(4)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
+            if (pending) {
+                put16(stlo + 48, st0);
+                put16(stlo + 32, st1);
+                put16(stlo + 16, st2);
+                put16(stlo, st3);
+            }
+            // <= 4 chunks still unread: the next 64-B segment fits the 8-chunk ring
+            const uint32_t occ = ((cons - 1 - (uint32_t)lo) >> 4) + 1;
+            pending = occ <= 4;
+            if (pending) {
+                asm_load16(st0, clampa(lo - 16));
+                asm_load16(st1, clampa(lo - 32));
+                asm_load16(st2, clampa(lo - 48));
+                asm_load16(st3, clampa(lo - 64));
+                lo -= 64;
+                stlo = (uint32_t)lo;
+            }
         }
         const bool full = k0 + DTILE < cmax;  // every row of the tile is complete for every stream
         if (full) {
@@ -915,8 +960,10 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
                 uint32_t wd = 0;
                 step(SEL0, wd);
                 step(SEL1, wd);
+                refill();
                 step(SEL2, wd);
                 step(SEL3, wd);
+                refill();
                 const uint32_t t2 = quad_t(wd);
                 if (s0 < N) *reinterpret_cast<uint32_t *>(rowp) = t2;
                 rowp += 4 * (uint64_t)N;
@@ -933,6 +980,7 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
                         nbits_snap = nbits;
                     }
                     step(sels[j], wd);
+                    if (j & 1) refill();
                 }
                 const uint32_t t2 = quad_t(wd);
                 const uint64_t pos = (kg + q) * N + s0;
@@ -948,7 +996,7 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
         }
         prev_full = full;
     }
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1)::"memory");
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
     if (c == cmax && cmax % 4 == 0) {  // no step past the end was executed for this lane
         cons_snap = cons;
         nbits_snap = nbits;
