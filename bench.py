@@ -36,8 +36,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
-    p.add_argument("--workload", default="rans", choices=["rans", "fse"],
-                   help="rans = BASELINE metric (configs[1]); fse = configs[2] (secondary line)")
+    p.add_argument("--workload", default="rans", choices=["rans", "fse", "o1", "blob"],
+                   help="rans = BASELINE metric (configs[1]); fse = configs[2]; o1 = configs[3] "
+                        "(per-GPU shard); blob = configs[4] (per-GPU batch) -- secondary lines")
+    p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--fse-block-kib", type=int, default=64)
     return p.parse_args()
 
@@ -191,6 +193,128 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
     return res
 
 
+def _timed(torch, dist, world, dev, fn, steps, warmup):
+    from zipora_amd import dist as zd
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    return zd.max_over_ranks(time.perf_counter() - t0, dev)
+
+
+def _line(metric, value, world, args, dt, data, config, roofline, extra):
+    r = {"metric": metric, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": data, "config": config,
+         "roofline": roofline}
+    r.update(extra)
+    return r
+
+
+def run_o1(args, torch, dist, world, rank, dev, zr, L):
+    """configs[3] per GPU: 128 MiB text-like shard (1 GiB over 8 GPUs), order-1
+    ContextualHuffman encode + decode (identity coding: two HBM copies)."""
+    from zipora_amd import dist as zd
+    n = 128 << 20
+    host = zr.synth("t", n, seed=zd.shard_seed(1, rank))
+    raw = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+    enc_model = zr.ContextualHuffmanEncoder(host[:1 << 16], zr.HuffmanOrder.Order1)
+    d = zr.HuffmanO1Device(enc_model)
+    enc = torch.empty_like(raw)
+    out = torch.empty_like(raw)
+
+    def step():
+        d.encode_async(raw, enc)
+        d.decode_async(enc, out, n)
+
+    L.zr_timer_reset()
+    L.zr_timer_enable(1)
+    dt = _timed(torch, dist, world, dev, step, args.steps, args.warmup)
+    L.zr_timer_enable(0)
+    if not torch.equal(out, raw):
+        raise SystemExit("O1 round trip mismatch")
+    ems, _ = kernel_ms(L, "huff_o1_encode")
+    dms, _ = kernel_ms(L, "huff_o1_decode")
+    ach = 2 * n / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
+    return _line("GiB/s encode+decode (device-resident), Huffman O1, 1 GiB text over 8 GPUs", world * n * args.steps
+                 / dt / 2**30, world, args, dt, "synthetic (order-1 Markov text, seed per rank)",
+                 {"workload": "ContextualHuffman order-1 encode+decode, 128 MiB text per GPU (1/8 of 1 GiB)",
+                  "parallelism": f"shard{world}"},
+                 {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_copy16 (huff_o1_decode)",
+                  "bytes_per_launch": 2 * n, "avg_launch_ms": round(dms, 4)},
+                 {"kernels_ms": {"huff_o1_encode": round(ems, 4), "huff_o1_decode": round(dms, 4)}})
+
+
+def run_blob(args, torch, dist, world, rank, dev, zr, L):
+    """configs[4] per GPU: R x 1 KiB text records, rANS x1 per record with a
+    shared trained table (RansBlobStore / RansCompressor record codec)."""
+    from zipora_amd import dist as zd
+    from zipora_amd.device import RansDeviceBatch
+    R, rl = args.records, 1024
+    total = R * rl
+    host = zr.synth("t", total, seed=zd.shard_seed(5, rank))
+    raw = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+    bt = RansDeviceBatch([rl] * R, 1, device=dev, shared_table=True)
+    enc = bt.new_enc()
+    out = bt.new_raw()
+
+    def step():
+        bt.histogram(raw)
+        zd.allreduce_histogram(bt.hist)
+        bt.tables_from_hist()
+        bt.encode(raw, enc)
+        bt.decode(enc, out)
+
+    L.zr_timer_reset()
+    L.zr_timer_enable(1)
+    dt = _timed(torch, dist, world, dev, step, args.steps, args.warmup)
+    L.zr_timer_enable(0)
+    bt.raise_on_error()
+    if not torch.equal(out, raw):
+        raise SystemExit("blob round trip mismatch")
+    comp = int(bt.enc_len.sum().item())
+    dms, _ = kernel_ms(L, "rans_decode_x1")
+    ems, _ = kernel_ms(L, "rans_encode_x1")
+    extra = {"kernels_ms": {"rans_encode_x1": round(ems, 4), "rans_decode_x1": round(dms, 4)},
+             "compressed_bytes": comp, "ratio": round(comp / total, 5)}
+    if world == 1 and not args.no_host_path:
+        # end to end from host memory: H2D records, code, D2H encoded, H2D encoded, decode, D2H records
+        pin = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        pin.copy_(raw.cpu())
+        penc = torch.empty(enc.numel(), dtype=torch.uint8, pin_memory=True)
+        pout = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+
+        def e2e():
+            raw.copy_(pin, non_blocking=True)
+            bt.histogram(raw)
+            bt.tables_from_hist()
+            bt.encode(raw, enc)
+            penc.copy_(enc, non_blocking=True)
+            enc.copy_(penc, non_blocking=True)
+            bt.decode(enc, out)
+            pout.copy_(out, non_blocking=True)
+
+        e2e_dt = _timed(torch, dist, world, dev, e2e, max(1, min(3, args.steps)), 1)
+        extra["host_resident_gibps"] = round(total * max(1, min(3, args.steps)) / e2e_dt / 2**30, 3)
+    ach = (comp + total) / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
+    return _line("GiB/s encode+decode (device-resident), rANS x1 record batch, 1 M x 1 KiB", world * total *
+                 args.steps / dt / 2**30, world, args, dt, "synthetic (order-1 Markov text records)",
+                 {"workload": f"{R} x 1 KiB records per GPU, rANS x1 per record, shared trained table",
+                  "records": R, "parallelism": f"shard{world}"},
+                 {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_dec_x1 (rans_decode_x1)",
+                  "bytes_per_launch": comp + total, "avg_launch_ms": round(dms, 4)}, extra)
+
+
 def main():
     args = parse()
     import torch
@@ -210,8 +334,9 @@ def main():
     L = zr.load()
     L.zr_set_device(local)
 
-    if args.workload == "fse":
-        res = run_fse(args, torch, dist, world, rank, dev, zr, L)
+    if args.workload in ("fse", "o1", "blob"):
+        fn = {"fse": run_fse, "o1": run_o1, "blob": run_blob}[args.workload]
+        res = fn(args, torch, dist, world, rank, dev, zr, L)
         if rank == 0:
             print(json.dumps(res), flush=True)
         if world > 1:
