@@ -776,20 +776,14 @@ __global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw
 //     (x >= 16 after a decode), so one 32-bit refill per PAIR of steps keeps
 //     it >= 32 bits at every pair start; the next dword is prefetched from the
 //     ring one pair ahead.
-//   * output: 4 steps per lane are packed into a dword and 4x4-byte
-//     transposed across each lane quad with DPP, so every lane stores one
-//     aligned dword per 4 steps: row k+q, streams s0..s0+3.
+//   * output: step k of stream s is byte k*N + s, so at every step a wave
+//     stores 64 consecutive bytes (one coalesced byte-store instruction, row
+//     base in SGPRs, no VALU work).
 // ----------------------------------------------------------------------
 constexpr int FW = 512;
 constexpr int RSLOTS = 8;
 constexpr int DTILE = 16;
 
-__device__ __forceinline__ uint32_t dpp_xor2(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
-}
-__device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
-}
 
 __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
                                                  uint32_t nblkF) {
@@ -824,8 +818,7 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
     const uint64_t off = base + inc - L + w.blockoff[(size_t)b * w.nblk + 2 * blkF];
     const uint64_t X = active ? ld_u64_u(e + 8 * (size_t)s) : RANS_L;
     uint8_t *outb = raw + a.raw_off[b];
-    const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24) && (N & 3) == 0 &&
-                      (((uintptr_t)outb) & 3) == 0;
+    const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24);
     if (!fast) atomicOr(flag, 1u);
     __syncthreads();
     const uint32_t any_slow = *flag;
@@ -888,11 +881,6 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
     v4u st0 = {0, 0, 0, 0}, st1 = st0, st2 = st0, st3 = st0;
     bool pending = false;
     uint32_t stlo = 0;
-    // quad transpose selectors
-    const uint32_t q = tid & 3;
-    const uint32_t sel1 = q < 2 ? 0x05040100u : 0x03020706u;
-    const uint32_t sel2 = (q & 1) ? 0x03070105u : 0x06020400u;
-    const uint64_t s0 = s & ~3u;
     const bool wave_live = (uint64_t)blkF * FW + (tid & ~63u) < N;  // wave-uniform
 
     // one 32-bit refill (branchless), then prefetch the next ring dword
@@ -906,8 +894,9 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
     refill();  // >= 32 bits before the first pair
     uint32_t cons_snap = cons;
     uint32_t nbits_snap = nbits;
-    // one decode step: renormalise (rans.rs:479-485) then decode (rans.rs:488-504)
-    auto step = [&](const uint32_t selj, uint32_t &wd) {
+    // one decode step: renormalise (rans.rs:479-485) then decode (rans.rs:488-504);
+    // returns the slot entry (its low byte is the symbol)
+    auto step = [&]() -> uint32_t {
         // x in [16, 2^24) needs 0, 1 or 2 bytes; the shift is 8 * #bytes
         const uint32_t sh8 = (__builtin_clz(x) & 24) - 8;
         x = (uint32_t)(((((uint64_t)x) << 32) | (uint32_t)(win >> 32)) << sh8 >> 32);
@@ -915,23 +904,20 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
         nbits -= sh8;
         const uint32_t ent = stab[x & (TOTFREQ - 1)];
         x = __umul24(ent >> 20, x >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
-        wd = __builtin_amdgcn_perm(ent, wd, selj);
+        return ent;
     };
-    // 4x4 byte transpose across the lane quad: lane q gets row kg+q of streams s0..s0+3
-    auto quad_t = [&](uint32_t wd) -> uint32_t {
-        const uint32_t t1 = __builtin_amdgcn_perm(dpp_xor2(wd), wd, sel1);
-        return __builtin_amdgcn_perm(dpp_xor1(t1), t1, sel2);
-    };
-    constexpr uint32_t SEL0 = 0x03020104u, SEL1 = 0x03020400u, SEL2 = 0x03040100u, SEL3 = 0x04020100u;
+    // output: at step k the wave's lanes write bytes k*N + s .. +63 -- one
+    // coalesced 64-byte byte-store per wave per step, row base in SGPRs
+    const bool wave_all = (uint64_t)blkF * FW + (tid & ~63u) + 64 <= N;  // wave-uniform
 
     bool prev_full = true;
     for (uint64_t k0 = 0; k0 < cmax; k0 += DTILE) {
         // ---- ring maintenance (wave-uniform position, per-lane masks)
         if (k0 > 0) {
-            // the previous boundary's segment loads are followed by exactly 4 dword
-            // stores of this wave when that tile was full and the wave is live
+            // the previous boundary's segment loads are followed by exactly DTILE
+            // byte stores of this wave when that tile was full and the wave is live
             if (prev_full && wave_live)
-                asm volatile("s_waitcnt vmcnt(4)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
+                asm volatile("s_waitcnt vmcnt(16)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
             else
                 asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
             if (pending) {
@@ -953,51 +939,37 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
             }
         }
         const bool full = k0 + DTILE < cmax;  // every row of the tile is complete for every stream
-        if (full) {
-            uint8_t *rowp = outb + (k0 + q) * N + s0;
+        if (full && wave_all) {
 #pragma unroll
-            for (int g = 0; g < DTILE / 4; g++) {
-                uint32_t wd = 0;
-                step(SEL0, wd);
-                step(SEL1, wd);
-                refill();
-                step(SEL2, wd);
-                step(SEL3, wd);
-                refill();
-                const uint32_t t2 = quad_t(wd);
-                if (s0 < N) *reinterpret_cast<uint32_t *>(rowp) = t2;
-                rowp += 4 * (uint64_t)N;
+            for (int j = 0; j < DTILE; j++) {
+                const uint32_t ent = step();
+                if (j & 1) refill();
+                (outb + (k0 + j) * N)[s] = (uint8_t)ent;
+            }
+        } else if (full) {
+#pragma unroll
+            for (int j = 0; j < DTILE; j++) {
+                const uint32_t ent = step();
+                if (j & 1) refill();
+                if (active) (outb + (k0 + j) * N)[s] = (uint8_t)ent;
             }
         } else {
             const uint32_t nsteps = (uint32_t)(cmax - k0);
-            for (uint32_t g = 0; g * 4 < nsteps; g++) {
-                const uint64_t kg = k0 + 4 * g;
-                uint32_t wd = 0;
-                const uint32_t sels[4] = {SEL0, SEL1, SEL2, SEL3};
-                for (int j = 0; j < 4; j++) {
-                    if (kg + j == c) {  // first step past this lane's symbols
-                        cons_snap = cons;
-                        nbits_snap = nbits;
-                    }
-                    step(sels[j], wd);
-                    if (j & 1) refill();
+            for (uint32_t j = 0; j < nsteps; j++) {
+                const uint64_t k = k0 + j;
+                if (k == c) {  // first step past this lane's symbols
+                    cons_snap = cons;
+                    nbits_snap = nbits;
                 }
-                const uint32_t t2 = quad_t(wd);
-                const uint64_t pos = (kg + q) * N + s0;
-                if (s0 < N) {
-                    if (pos + 4 <= n) {
-                        *reinterpret_cast<uint32_t *>(outb + pos) = t2;
-                    } else {
-                        for (uint32_t j = 0; j < 4; j++)
-                            if (pos + j < n) outb[pos + j] = (uint8_t)(t2 >> (8 * j));
-                    }
-                }
+                const uint32_t ent = step();
+                if (j & 1) refill();
+                if (k < c) (outb + k * N)[s] = (uint8_t)ent;
             }
         }
         prev_full = full;
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
-    if (c == cmax && cmax % 4 == 0) {  // no step past the end was executed for this lane
+    if (c == cmax) {  // no step past the end was executed for this lane
         cons_snap = cons;
         nbits_snap = nbits;
     }
