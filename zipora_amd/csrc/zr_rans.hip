@@ -239,14 +239,16 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
     if (single_mode(n, N)) return;
-    // per symbol: x = xmax = freq << 12 (0 = not in table), y = start,
-    // z = reciprocal, w = (4096 - freq) | rsh << 16
+    // per symbol: x = xmax = freq << 12 (0 = not in table), y = xmax << 8 (two
+    // renorm bytes at or above it), z = reciprocal,
+    // w = start | (4096 - freq) << 12 | rsh << 24
     __shared__ uint4 et[256];
     __shared__ unsigned long long sh[4];
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
     {
         const uint32_t v = threadIdx.x, f = T->freq[v];
-        et[v] = make_uint4(f << TF_SHIFT, T->start[v], T->rcp[v], (TOTFREQ - f) | (T->rsh[v] << 16));
+        et[v] = make_uint4(f << TF_SHIFT, f >= TOTFREQ ? 0xFFFFFFFFu : f << (TF_SHIFT + 8), T->rcp[v],
+                           T->start[v] | (((TOTFREQ - f) & 0xFFF) << 12) | (T->rsh[v] << 24));
     }
     __syncthreads();
     // Input rows k*N + 256*blk .. +255 are staged through an LDS tile of ETILE rows:
@@ -284,21 +286,25 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     bool err = false;
     // encode_symbol (rans.rs:303-335), branchless: at most two renorm bytes
     // (x < 2^24, xmax >= 2^12); q = x / f by the exact 24-bit reciprocal.
-    auto enc_step = [&](const uint4 e, bool valid) {
-        const uint32_t xmax = e.x;  // ((L << 8) / TOTFREQ) * freq (rans.rs:319)
-        err |= valid && xmax == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
-        const bool c1 = valid && x >= xmax;
-        const uint32_t b1 = x & 0xFF;
-        uint32_t y = c1 ? x >> 8 : x;
-        const bool c2 = valid && y >= xmax;
-        const uint32_t b2 = y & 0xFF;
-        y = c2 ? y >> 8 : y;
-        const uint32_t nb = (c1 ? 8u : 0u) + (c2 ? 8u : 0u);
-        const uint32_t bytes = __builtin_amdgcn_ubfe(b1 | (b2 << 8), 0, nb);
-        acc |= (uint64_t)bytes << nacc;
+    // renorm bytes: x >= xmax << 8 -> 2, x >= xmax -> 1 (y >> 8 >= xmax <=> y >= xmax << 8)
+    uint32_t xmin = 0xFFFFFFFFu;  // min xmax over coded symbols: 0 = a symbol not in the table
+    auto enc_fast = [&](const uint4 e) {
+        xmin = min(xmin, e.x);
+        const uint32_t nb = x >= e.y ? 16u : (x >= e.x ? 8u : 0u);
+        acc |= (uint64_t)__builtin_amdgcn_ubfe(x, 0, nb) << nacc;
         nacc += nb;
-        const uint32_t q = __umulhi(y << 8, e.z) >> (e.w >> 16);  // y / f
-        const uint32_t xn = y + e.y + __umul24(q, e.w & 0xFFFF);  // (y/f)*4096 + y%f + start
+        const uint32_t y = x >> nb;
+        const uint32_t q = __umulhi(y << 8, e.z) >> (e.w >> 24);          // y / f
+        x = y + (e.w & 0xFFF) + __umul24(q, (e.w >> 12) & 0xFFF);         // (y/f)*4096 + y%f + start
+    };
+    auto enc_step = [&](const uint4 e, bool valid) {
+        err |= valid && e.x == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
+        const uint32_t nb = valid ? (x >= e.y ? 16u : (x >= e.x ? 8u : 0u)) : 0u;
+        acc |= (uint64_t)__builtin_amdgcn_ubfe(x, 0, nb) << nacc;
+        nacc += nb;
+        const uint32_t y = x >> nb;
+        const uint32_t q = __umulhi(y << 8, e.z) >> (e.w >> 24);
+        const uint32_t xn = y + (e.w & 0xFFF) + __umul24(q, (e.w >> 12) & 0xFFF);
         x = valid ? xn : x;
     };
     uint32_t sc = 0;  // store instructions this wave issued since the last piece load
@@ -368,7 +374,22 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         sc = 0;
         if (t > 0) issue_piece(t - 1, pend);
         const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
-        if (rtop == ETILE && t * ETILE + ETILE < cmax) {
+        const bool wave_all = (uint64_t)blk * 256 + (threadIdx.x & ~63u) + 64 <= N;  // wave-uniform
+        if (rtop == ETILE && t * ETILE + ETILE < cmax && wave_all) {
+            // full tile, every lane of the wave a stream: no per-lane predicates
+#pragma unroll
+            for (int g = ETILE - 4; g >= 0; g -= 4) {
+                const uint32_t s3 = itile[(g + 3) * 256 + threadIdx.x], s2 = itile[(g + 2) * 256 + threadIdx.x];
+                const uint32_t s1 = itile[(g + 1) * 256 + threadIdx.x], s0 = itile[g * 256 + threadIdx.x];
+                const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
+                enc_fast(e3);
+                enc_fast(e2);
+                flush();
+                enc_fast(e1);
+                enc_fast(e0);
+                flush();
+            }
+        } else if (rtop == ETILE && t * ETILE + ETILE < cmax) {
             // full tile: every row is complete for every stream (rows < cmax - 1)
 #pragma unroll
             for (int g = ETILE - 4; g >= 0; g -= 4) {
@@ -402,7 +423,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     }
     if (nacc) out[nout] = (uint32_t)acc;
     const uint32_t nacc_bytes = nacc / 8;
-    if (err) atomicOr(&a.status[b], 1);  // marked; converted to ZR_INVALID_INPUT by the scan
+    if (err || xmin == 0) atomicOr(&a.status[b], 1);  // marked; converted to ZR_INVALID_INPUT by the scan
     const uint32_t bytes = nout * 4 + nacc_bytes;
     if (active) {
         w.st_state[(size_t)b * N + s] = x;
