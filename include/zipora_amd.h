@@ -70,7 +70,9 @@ int32_t zr_rans_decode(const zr_rans_table *t, uint32_t n_streams, const uint8_t
  *   enc_len[b]         : encoded length (written by encode, read by decode)
  *   status[b]          : ZR_OK or ZR_INVALID_INPUT (written by both)
  * Tables are device tables (zr_rans_dtab_bytes() each); table_stride is 0 when
- * every buffer shares table 0, 1 when buffer b uses table b. */
+ * every buffer shares table 0, 1 when buffer b uses table b. min_len is a
+ * host-side lower bound of the lengths (0 = unknown): when it is >= n_streams
+ * > 1 no buffer takes the x1 layout and its kernels are not launched. */
 typedef struct {
     uint32_t n_buffers;
     uint32_t n_streams;
@@ -82,6 +84,7 @@ typedef struct {
     int32_t *status;
     const void *tables;
     uint32_t table_stride;
+    uint64_t min_len;
 } zr_rans_batch;
 
 size_t zr_rans_dtab_bytes(void);

@@ -32,7 +32,7 @@ class RansBatch(ctypes.Structure):
     _fields_ = [("n_buffers", ctypes.c_uint32), ("n_streams", ctypes.c_uint32),
                 ("max_len", ctypes.c_uint64), ("len", c_vp), ("raw_off", c_vp),
                 ("enc_off", c_vp), ("enc_len", c_vp), ("status", c_vp), ("tables", c_vp),
-                ("table_stride", ctypes.c_uint32)]
+                ("table_stride", ctypes.c_uint32), ("min_len", ctypes.c_uint64)]
 
 
 class FseConfig(ctypes.Structure):

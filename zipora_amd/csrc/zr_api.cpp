@@ -251,6 +251,7 @@ int32_t run_single(bool encode, const zr_rans_table *t, uint32_t N, const uint8_
     bt.status = reinterpret_cast<int32_t *>(m + 4);
     bt.tables = d_tab.p;
     bt.table_stride = 0;
+    bt.min_len = raw_len;
     int32_t st;
     if (encode) {
         if (in_len) ZR_HIP(hipMemcpy(d_raw.p, in, in_len, hipMemcpyHostToDevice));

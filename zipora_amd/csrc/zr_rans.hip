@@ -1156,8 +1156,10 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         timer_end("rans_compact", s);
     }
     timer_begin("rans_encode_x1", s);
-    hipLaunchKernelGGL(k_enc_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, raw, a, w);
-    hipLaunchKernelGGL(k_enc_x1_compact, dim3(a.B), dim3(64), 0, s, enc, a, w);
+    if (!(bt->min_len >= a.N && a.N > 1)) {  // some buffer may take the x1 layout
+        hipLaunchKernelGGL(k_enc_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, raw, a, w);
+        hipLaunchKernelGGL(k_enc_x1_compact, dim3(a.B), dim3(64), 0, s, enc, a, w);
+    }
     timer_end("rans_encode_x1", s);
     ZR_HIP(hipGetLastError());
     return ZR_OK;
@@ -1187,7 +1189,8 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
         hipLaunchKernelGGL(k_dec_xn<true>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
     }
     timer_begin("rans_decode_x1", s);
-    hipLaunchKernelGGL(k_dec_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, enc, raw, a);
+    if (!(bt->min_len >= a.N && a.N > 1))
+        hipLaunchKernelGGL(k_dec_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, enc, raw, a);
     timer_end("rans_decode_x1", s);
     ZR_HIP(hipGetLastError());
     return ZR_OK;

@@ -68,6 +68,7 @@ class RansDeviceBatch:
         c.enc_len, c.status = self.enc_len.data_ptr(), self.status.data_ptr()
         c.tables = self.tables.data_ptr()
         c.table_stride = 0 if self.shared else 1
+        c.min_len = min(lens) if lens else 0
 
     # ---- areas
     def new_raw(self):
