@@ -109,10 +109,10 @@ def test_rans_decode_crafted_streams_match_oracle(zr, oracle):
             assert got == ref, f"N={N} trial={trial}"
 
 
-def _batch_roundtrip(zr, oracle, lens, N, kind, shared):
+def _batch_roundtrip(zr, oracle, lens, N, kind, shared, align=16):
     import torch
     from zipora_amd.device import RansDeviceBatch
-    bt = RansDeviceBatch(lens, N, shared_table=shared)
+    bt = RansDeviceBatch(lens, N, shared_table=shared, align=align)
     raw = bt.new_raw()
     datas = []
     for b, n in enumerate(lens):
@@ -154,6 +154,9 @@ def test_rans_device_batch_text_zipf(zr, oracle):
 def test_rans_blob_batch_x1(zr, oracle):
     """config-5 shape in miniature: many 1 KiB records, x1 each, shared trained table."""
     _batch_roundtrip(zr, oracle, [1024] * 300 + [17, 0, 2000], 1, "t", True)
+    # unaligned record offsets (byte-granular layouts) take the byte-store paths
+    _batch_roundtrip(zr, oracle, [1000, 3, 1021, 16, 15, 777], 1, "z", True, align=1)
+    _batch_roundtrip(zr, oracle, [1000, 3, 1021, 16, 15, 777], 1, "z", False, align=1)
 
 
 def test_rans_full_size_property(zr, oracle):

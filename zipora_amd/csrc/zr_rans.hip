@@ -82,19 +82,7 @@ struct KArgs {  // kernel-side copy of zr_rans_batch
 // histogram (the callers' [u32;256] counts: compression/mod.rs:433-436,
 // blob_store/entropy.rs:213-216, rans.rs:708-714)
 // ======================================================================
-__global__ __launch_bounds__(256) void k_hist(const uint8_t *raw, KArgs a, int shared,
-                                              uint32_t *hist, uint64_t chunk, uint32_t nchunk) {
-    const uint32_t b = blockIdx.x / nchunk, c = blockIdx.x % nchunk;
-    if (b >= a.B) return;
-    const uint64_t n = a.len[b];
-    const uint64_t lo = (uint64_t)c * chunk;
-    if (lo >= n) return;
-    const uint64_t hi = min(n, lo + chunk);
-    __shared__ uint32_t h[4][257];
-    for (int i = threadIdx.x; i < 4 * 257; i += 256) (&h[0][0])[i] = 0;
-    __syncthreads();
-    uint32_t *mine = h[threadIdx.x >> 6];
-    const uint8_t *p = raw + a.raw_off[b];
+__device__ __forceinline__ void hist_range(const uint8_t *p, uint64_t lo, uint64_t hi, uint32_t *mine) {
     // head bytes up to 16-byte alignment
     const uint64_t mis = (16 - (((uintptr_t)(p + lo)) & 15)) & 15;
     const uint64_t body_lo = min(hi, lo + mis);
@@ -114,10 +102,36 @@ __global__ __launch_bounds__(256) void k_hist(const uint8_t *raw, KArgs a, int s
     }
     const uint64_t tail_lo = body_lo + units * 16;
     if (threadIdx.x < hi - tail_lo) atomicAdd(&mine[p[tail_lo + threadIdx.x]], 1u);
+}
+
+// Work item = (buffer, 64 KiB chunk). Per-buffer histograms: one workgroup
+// per item. Shared histogram: a grid-stride loop over the items with one LDS
+// histogram per workgroup and one global add per bin at the end (a batch of
+// a million 1 KiB records would otherwise send a global atomic per bin per
+// record to the same 256 counters).
+__global__ __launch_bounds__(256) void k_hist(const uint8_t *raw, KArgs a, int shared,
+                                              uint32_t *hist, uint64_t chunk, uint32_t nchunk) {
+    __shared__ uint32_t h[4][257];
+    for (int i = threadIdx.x; i < 4 * 257; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t *mine = h[threadIdx.x >> 6];
+    const uint64_t items = (uint64_t)a.B * nchunk;
+    const uint64_t step = shared ? gridDim.x : items;
+    for (uint64_t it = blockIdx.x; it < items; it += step) {
+        const uint32_t b = (uint32_t)(it / nchunk), c = (uint32_t)(it % nchunk);
+        const uint64_t n = a.len[b];
+        const uint64_t lo = (uint64_t)c * chunk;
+        if (lo >= n) continue;
+        hist_range(raw + a.raw_off[b], lo, min(n, lo + chunk), mine);
+        if (!shared) break;
+    }
     __syncthreads();
     const uint32_t v = threadIdx.x;
     const uint32_t s = h[0][v] + h[1][v] + h[2][v] + h[3][v];
-    if (s) atomicAdd(&hist[(shared ? 0 : (size_t)b * 256) + v], s);
+    if (s) {
+        const uint32_t b = (uint32_t)(blockIdx.x / nchunk);
+        atomicAdd(&hist[(shared ? 0 : (size_t)b * 256) + v], s);
+    }
 }
 
 // ======================================================================
@@ -436,7 +450,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
 // ======================================================================
 // encode/decode, x1 layout: one lane per buffer (encode_single rans.rs:354-366)
 // ======================================================================
-__global__ __launch_bounds__(64) void k_enc_x1(const uint8_t *raw, KArgs a, RansWork w) {
+__global__ __launch_bounds__(64) void k_enc_x1_generic(const uint8_t *raw, KArgs a, RansWork w) {
     const uint32_t b = blockIdx.x * 64 + threadIdx.x;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
@@ -1001,7 +1015,7 @@ __global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *ra
     }
 }
 
-__global__ __launch_bounds__(64) void k_dec_x1(const uint8_t *enc, uint8_t *raw, KArgs a) {
+__global__ __launch_bounds__(64) void k_dec_x1_generic(const uint8_t *enc, uint8_t *raw, KArgs a) {
     const uint32_t b = blockIdx.x * 64 + threadIdx.x;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
@@ -1029,6 +1043,206 @@ __global__ __launch_bounds__(64) void k_dec_x1(const uint8_t *enc, uint8_t *raw,
         const uint32_t sy = T->slot[slot] & 0xFF;
         X = (uint64_t)T->freq[sy] * (X >> TF_SHIFT) + slot - T->start[sy];
         out[i] = (uint8_t)sy;
+    }
+}
+
+// ----------------------------------------------------------------------
+// x1 layout, shared table (record batches: RansBlobStore / RansCompressor
+// records). One lane per buffer, 256 buffers per
+// workgroup sharing the LDS table. Input and output move in 16-byte chunks
+// (the generic kernels above move single bytes with global table reads).
+// The encoder writes straight into the final "bytes || state" layout: its
+// destination offset is known before encoding, so x1 needs no compaction.
+// ----------------------------------------------------------------------
+typedef unsigned x4u __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t *enc, KArgs a, RansWork w) {
+    __shared__ uint4 et[256];
+    const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
+    {
+        const uint32_t v = threadIdx.x, f = T->freq[v];
+        et[v] = make_uint4(f << TF_SHIFT, f >= TOTFREQ ? 0xFFFFFFFFu : f << (TF_SHIFT + 8), T->rcp[v],
+                           T->start[v] | (((TOTFREQ - f) & 0xFFF) << 12) | (T->rsh[v] << 24));
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    if (!single_mode(n, a.N)) return;
+    const uint8_t *in = raw + a.raw_off[b];
+    uint8_t *out = enc + a.enc_off[b];
+    const bool vec_out = (((uintptr_t)out) & 15) == 0;
+    uint32_t x = RANS_L;
+    uint32_t xmin = 0xFFFFFFFFu;
+    uint64_t acc = 0;
+    uint32_t nacc = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0;
+    uint64_t nout = 0;  // bytes stored
+    auto enc_step = [&](const uint4 e) {  // rans.rs:303-335 (see k_enc_xn)
+        xmin = min(xmin, e.x);
+        const uint32_t nb = x >= e.y ? 16u : (x >= e.x ? 8u : 0u);
+        acc |= (uint64_t)__builtin_amdgcn_ubfe(x, 0, nb) << nacc;
+        nacc += nb;
+        const uint32_t y = x >> nb;
+        const uint32_t q = __umulhi(y << 8, e.z) >> (e.w >> 24);
+        x = y + (e.w & 0xFFF) + __umul24(q, (e.w >> 12) & 0xFFF);
+    };
+    auto push = [&]() {  // move whole dwords of acc to the queue, 16 bytes to memory
+        if (nacc >= 32) {
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            q3 = (uint32_t)acc;
+            acc >>= 32;
+            nacc -= 32;
+            if (++nq == 4) {
+                if (vec_out) {
+                    *reinterpret_cast<x4u *>(out + nout) = x4u{q0, q1, q2, q3};
+                } else {
+                    const uint32_t qs[4] = {q0, q1, q2, q3};
+                    for (int i = 0; i < 16; i++) out[nout + i] = (uint8_t)(qs[i >> 2] >> (8 * (i & 3)));
+                }
+                nout += 16;
+                nq = 0;
+            }
+        }
+    };
+    const uint64_t full = n & ~15ull;
+    for (uint64_t i = n; i > full;) {  // ragged top, < 16 symbols
+        enc_step(et[in[--i]]);
+        push();
+    }
+    if (full) {
+        int64_t c = (int64_t)(full >> 4) - 1;
+        if ((((uintptr_t)in) & 15) == 0) {
+            const x4u *in4 = reinterpret_cast<const x4u *>(in);
+            const x4u z = {0, 0, 0, 0};
+            x4u cur = in4[c];
+            x4u n1 = c >= 1 ? in4[c - 1] : z;
+            for (; c >= 0; c--) {
+                const x4u wv = cur;
+                cur = n1;
+                if (c >= 2) n1 = in4[c - 2];
+                uint4 e[16];
+#pragma unroll
+                for (int k = 15; k >= 0; k--) e[k] = et[(wv[k >> 2] >> (8 * (k & 3))) & 0xFF];
+#pragma unroll
+                for (int k = 15; k >= 0; k--) {
+                    enc_step(e[k]);
+                    if (k & 1) push();
+                }
+                push();
+            }
+        } else {
+            for (uint64_t i = full; i-- > 0;) {
+                enc_step(et[in[i]]);
+                push();
+            }
+        }
+    }
+    // drain: queued dwords, the partial dword, then the u64 state
+    {
+        const uint32_t qs[4] = {q0, q1, q2, q3};
+        for (uint32_t i = 0; i < nq; i++) {
+            const uint32_t d = qs[4 - nq + i];
+            for (int t = 0; t < 4; t++) out[nout + 4 * i + t] = (uint8_t)(d >> (8 * t));
+        }
+        nout += 4 * nq;
+    }
+    for (uint32_t t = 0; t < nacc / 8; t++) out[nout + t] = (uint8_t)(acc >> (8 * t));
+    nout += nacc / 8;
+    for (int t = 0; t < 8; t++) out[nout + t] = (uint8_t)((uint64_t)x >> (8 * t));
+    if (xmin == 0 && n) a.status[b] = ZR_INVALID_INPUT;  // "Symbol {} not in frequency table"
+    a.enc_len[b] = nout + 8;
+}
+
+// rans.rs:523-560 decode_single: state = last 8 bytes; renormalisation bytes
+// are read backwards from len - 8 through a 16-byte register window
+__global__ __launch_bounds__(256) void k_dec_x1_fast(const uint8_t *enc, uint8_t *raw, KArgs a) {
+    __shared__ uint32_t stab[TOTFREQ];
+    const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);
+    for (uint32_t j = threadIdx.x; j < TOTFREQ; j += 256) stab[j] = T->slot[j];
+    const bool single = T->kind != DT_NORMAL;  // single-symbol / empty tables: global reads
+    __syncthreads();
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    if (n == 0 || !single_mode(n, a.N)) return;
+    const uint64_t len = a.enc_len[b];
+    if (len < 8) {  // "rANS data too short" (rans.rs:524-526)
+        a.status[b] = ZR_INVALID_INPUT;
+        return;
+    }
+    const uint8_t *e = enc + a.enc_off[b];
+    uint64_t X = ld_u64_u(e + len - 8);
+    uint64_t pos = len - 8;  // bytes [0, pos) unread
+    // backward byte reader: chunk cur holds the aligned 16 bytes containing pos - 1
+    const x4u *e4 = reinterpret_cast<const x4u *>(e - (((uintptr_t)e) & 15));
+    const uint64_t ebias = ((uintptr_t)e) & 15;  // e[i] = bytes of e4 at ebias + i
+    int64_t cidx = ((int64_t)(pos + ebias) - 1) >> 4;
+    x4u cur = {0, 0, 0, 0};
+    if (pos) cur = e4[cidx];
+    auto rd = [&]() -> uint32_t {  // pos > 0: return e[--pos]
+        pos--;
+        const uint64_t ab = pos + ebias;
+        const int64_t ci = (int64_t)(ab >> 4);
+        if (ci != cidx) {
+            cidx = ci;
+            cur = e4[ci];
+        }
+        const uint32_t k = (uint32_t)(ab & 15);
+        const uint32_t dw = (k >> 2) == 0 ? cur.x : (k >> 2) == 1 ? cur.y : (k >> 2) == 2 ? cur.z : cur.w;
+        return (dw >> (8 * (k & 3))) & 0xFF;
+    };
+    uint8_t *out = raw + a.raw_off[b];
+    const bool vec_out = (((uintptr_t)out) & 15) == 0;
+    uint32_t w0 = 0, w1 = 0, w2 = 0, acc = 0;
+    bool err = false;
+    uint64_t i = 0;
+    for (; i < n; i++) {
+        // renormalise first (rans.rs:479-485)
+        while (X < RANS_L) {
+            if (pos == 0) {
+                err = true;
+                break;
+            }
+            X = (X << 8) | rd();
+        }
+        if (err) break;
+        uint32_t sy;
+        if (single) {
+            const uint32_t slot = (uint32_t)(X & (TOTFREQ - 1));
+            sy = T->slot[slot] & 0xFF;
+            X = (uint64_t)T->freq[sy] * (X >> TF_SHIFT) + slot - T->start[sy];
+        } else {
+            const uint32_t ent = stab[X & (TOTFREQ - 1)];
+            sy = ent & 0xFF;
+            X = (uint64_t)(ent >> 20) * (X >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
+        }
+        if (vec_out) {
+            acc = (acc >> 8) | (sy << 24);
+            if ((i & 15) == 15) {
+                *reinterpret_cast<x4u *>(out + i - 15) = x4u{w0, w1, w2, acc};
+            } else if ((i & 3) == 3) {
+                w0 = w1;
+                w1 = w2;
+                w2 = acc;
+            }
+        } else {
+            out[i] = (uint8_t)sy;
+        }
+    }
+    if (err) {
+        a.status[b] = ZR_INVALID_INPUT;  // "Insufficient data" (rans.rs:480-482)
+        return;
+    }
+    const uint32_t rem = (uint32_t)(n & 15);
+    if (vec_out && rem) {
+        const uint64_t g = n - rem;
+        const uint32_t cq = rem >> 2, r = rem & 3;
+        const uint32_t ws[3] = {w0, w1, w2};
+        for (uint32_t k = 0; k < cq; k++)
+            for (int t = 0; t < 4; t++) out[g + 4 * k + t] = (uint8_t)(ws[3 - cq + k] >> (8 * t));
+        for (uint32_t t = 0; t < r; t++) out[g + 4 * cq + t] = (uint8_t)(acc >> (8 * (4 - r + t)));
     }
 }
 
@@ -1110,7 +1324,8 @@ int32_t zr_histogram_dev(const uint8_t *raw, const zr_rans_batch *bt, int32_t sh
     KArgs a = kargs(bt);
     const uint64_t chunk = 64 * 1024;
     const uint32_t nchunk = (uint32_t)ceil_div(bt->max_len, chunk);
-    const uint64_t grid = (uint64_t)nchunk * a.B;
+    const uint64_t items = (uint64_t)nchunk * a.B;
+    const uint64_t grid = shared ? std::min<uint64_t>(items, 8192) : items;
     timer_begin("histogram", (hipStream_t)stream);
     hipLaunchKernelGGL(k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a,
                        shared, hist_dev, chunk, nchunk);
@@ -1157,8 +1372,12 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
     }
     timer_begin("rans_encode_x1", s);
     if (!(bt->min_len >= a.N && a.N > 1)) {  // some buffer may take the x1 layout
-        hipLaunchKernelGGL(k_enc_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, raw, a, w);
-        hipLaunchKernelGGL(k_enc_x1_compact, dim3(a.B), dim3(64), 0, s, enc, a, w);
+        if (a.table_stride == 0) {
+            hipLaunchKernelGGL(k_enc_x1_fast, dim3((uint32_t)ceil_div(a.B, 256)), dim3(256), 0, s, raw, enc, a, w);
+        } else {
+            hipLaunchKernelGGL(k_enc_x1_generic, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, raw, a, w);
+            hipLaunchKernelGGL(k_enc_x1_compact, dim3(a.B), dim3(64), 0, s, enc, a, w);
+        }
     }
     timer_end("rans_encode_x1", s);
     ZR_HIP(hipGetLastError());
@@ -1189,8 +1408,12 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
         hipLaunchKernelGGL(k_dec_xn<true>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
     }
     timer_begin("rans_decode_x1", s);
-    if (!(bt->min_len >= a.N && a.N > 1))
-        hipLaunchKernelGGL(k_dec_x1, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, enc, raw, a);
+    if (!(bt->min_len >= a.N && a.N > 1)) {
+        if (a.table_stride == 0)
+            hipLaunchKernelGGL(k_dec_x1_fast, dim3((uint32_t)ceil_div(a.B, 256)), dim3(256), 0, s, enc, raw, a);
+        else
+            hipLaunchKernelGGL(k_dec_x1_generic, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, enc, raw, a);
+    }
     timer_end("rans_decode_x1", s);
     ZR_HIP(hipGetLastError());
     return ZR_OK;
