@@ -219,6 +219,53 @@ def _line(metric, value, world, args, dt, data, config, roofline, extra):
     return r
 
 
+def _cpu_pool(fn, items, threads):
+    import concurrent.futures as cf
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(fn, items))
+    return time.perf_counter() - t0
+
+
+def cpu_baseline_o1(host, threads):
+    """Oracle ContextualHuffman order-1 (interleaved.rs) encode+decode, 4 MiB slices."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    O.lib()
+    sl = 4 << 20
+    ns = min(len(host) // sl, 2 * threads)
+
+    def one(i):
+        d = host[i * sl:(i + 1) * sl]
+        c = O.Ctx(d[:1 << 16], 1)
+        assert c.decode(c.encode(d), len(d)) == d
+
+    dt = _cpu_pool(one, range(ns), threads)
+    return {"value": round(ns * sl / 2**30 / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{ns} x 4 MiB slices of the same text, order-1 encode+decode, {threads} threads, "
+                      f"{dt:.2f} s"}
+
+
+def cpu_baseline_blob(host, threads):
+    """Oracle rANS x1 per 1 KiB record with one shared table (RansCompressor-style)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    O.lib()
+    per = 4096
+    nrec = min(len(host) // 1024, per * threads)
+    t = _table_fast(O, host[:nrec * 1024])
+
+    def one(k):
+        for r in range(k * per, min(nrec, (k + 1) * per)):
+            d = host[r * 1024:(r + 1) * 1024]
+            assert O.rans_decode(t, 1, O.rans_encode(t, 1, d), 1024) == d
+
+    dt = _cpu_pool(one, range((nrec + per - 1) // per), threads)
+    return {"value": round(nrec * 1024 / 2**30 / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{nrec} x 1 KiB records of the same batch, x1 encode+decode with one shared table, "
+                      f"{threads} threads, {dt:.2f} s"}
+
+
 def run_o1(args, torch, dist, world, rank, dev, zr, L):
     """configs[3] per GPU: 128 MiB text-like shard (1 GiB over 8 GPUs), order-1
     ContextualHuffman encode + decode (identity coding: two HBM copies)."""
@@ -244,14 +291,16 @@ def run_o1(args, torch, dist, world, rank, dev, zr, L):
     ems, _ = kernel_ms(L, "huff_o1_encode")
     dms, _ = kernel_ms(L, "huff_o1_decode")
     ach = 2 * n / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
+    extra = {"kernels_ms": {"huff_o1_encode": round(ems, 4), "huff_o1_decode": round(dms, 4)}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        extra["cpu_baseline"] = cpu_baseline_o1(host, args.cpu_threads)
     return _line("GiB/s encode+decode (device-resident), Huffman O1, 1 GiB text over 8 GPUs", world * n * args.steps
                  / dt / 2**30, world, args, dt, "synthetic (order-1 Markov text, seed per rank)",
                  {"workload": "ContextualHuffman order-1 encode+decode, 128 MiB text per GPU (1/8 of 1 GiB)",
                   "parallelism": f"shard{world}"},
                  {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_copy16 (huff_o1_decode)",
-                  "bytes_per_launch": 2 * n, "avg_launch_ms": round(dms, 4)},
-                 {"kernels_ms": {"huff_o1_encode": round(ems, 4), "huff_o1_decode": round(dms, 4)}})
+                  "bytes_per_launch": 2 * n, "avg_launch_ms": round(dms, 4)}, extra)
 
 
 def run_blob(args, torch, dist, world, rank, dev, zr, L):
@@ -305,6 +354,8 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
 
         e2e_dt = _timed(torch, dist, world, dev, e2e, max(1, min(3, args.steps)), 1)
         extra["host_resident_gibps"] = round(total * max(1, min(3, args.steps)) / e2e_dt / 2**30, 3)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        extra["cpu_baseline"] = cpu_baseline_blob(host, args.cpu_threads)
     ach = (comp + total) / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
     return _line("GiB/s encode+decode (device-resident), rANS x1 record batch, 1 M x 1 KiB", world * total *
                  args.steps / dt / 2**30, world, args, dt, "synthetic (order-1 Markov text records)",
