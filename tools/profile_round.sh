@@ -11,16 +11,19 @@ O=gpurun_out/prof_$R
 mkdir -p $O/summary
 B="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-path"
 BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-path"
-K="--kernel-include-regex k_dec_fast|k_enc_xn|k_enc_compact|k_hist|k_fse_dec|k_fse_enc|k_copy16"
+K="--kernel-include-regex k_dec_fast|k_enc_xn|k_enc_compact|k_hist|k_fse_dec|k_fse_enc|k_copy16|k_enc_x1_fast|k_dec_x1_fast"
 # 1. rANS (headline) kernel trace + stats, default bench command
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rans -o rans -- $B > $O/rans_bench.log 2>&1
 # 2. HBM traffic, one counter group per pass
 timeout -k 10 300 rocprofv3 $K --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o fetch -- $BP > $O/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 $K --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o write -- $BP > $O/pmc_write.log 2>&1
-# 3. FSE workload (configs[2]) kernel trace + stats
+# 3. FSE workload (configs[2]) kernel trace + stats and traffic
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/fse -o fse -- python3 bench.py --workload fse --steps 5 --warmup 2 --no-cpu-baseline > $O/fse_bench.log 2>&1
 timeout -k 10 300 rocprofv3 $K --pmc FETCH_SIZE --output-format csv -d $O/pmc_fse_fetch -o fetch -- python3 bench.py --workload fse --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_fse_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 $K --pmc WRITE_SIZE --output-format csv -d $O/pmc_fse_write -o write -- python3 bench.py --workload fse --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_fse_write.log 2>&1
+# 4. O1 shard (configs[3]) and record batch (configs[4]) kernel traces
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/o1 -o o1 -- python3 bench.py --workload o1 --steps 10 --warmup 3 --no-cpu-baseline > $O/o1_bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/blob -o blob -- python3 bench.py --workload blob --steps 3 --warmup 1 --no-cpu-baseline --no-host-path > $O/blob_bench.log 2>&1
 python3 tools/summarize_prof.py $O > $O/summary/summary.txt 2>&1 || true
-find $O -name "*kernel_stats.csv" -exec cp {} $O/summary/ \; || true
+for f in $(find $O -name "*kernel_stats.csv"); do cp $f $O/summary/; done
 ls -la $O/summary
