@@ -475,8 +475,8 @@ def main():
                    "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic("k_dec_fast")[0], "traffic_source": pmc_traffic("k_dec_fast")[1],
-                     "kernel": "k_dec_fast (rans_decode)",
+                     "traffic": pmc_traffic("k_dec_xn_fast")[0], "traffic_source": pmc_traffic("k_dec_xn_fast")[1],
+                     "kernel": "k_dec_xn_fast (rans_decode)",
                      "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
         "kernels_ms": {"rans_decode": round(dec_ms, 4), "rans_encode": round(enc_ms, 4),
                        "rans_compact": round(cmp_ms, 4), "histogram": round(hist_ms, 4)},

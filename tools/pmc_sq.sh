@@ -4,7 +4,7 @@ set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/sq
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-path"
-K="--kernel-include-regex k_dec_fast|k_enc_xn|k_enc_compact|k_hist"
+K="--kernel-include-regex k_dec_xn_fast|k_enc_xn|k_enc_compact|k_hist"
 timeout -k 10 300 rocprofv3 $K --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d gpurun_out/sq -o s1 -- $B > gpurun_out/sq/s1.log 2>&1
 timeout -k 10 300 rocprofv3 $K --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sq -o s2 -- $B > gpurun_out/sq/s2.log 2>&1
 ls gpurun_out/sq

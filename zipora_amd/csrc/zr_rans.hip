@@ -799,219 +799,274 @@ __global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw
 }
 
 // ----------------------------------------------------------------------
-// Fast xN decode. One lane = one stream, FW = 512 lanes per workgroup share
-// one 16 KiB LDS slot table (2 workgroups per CU hold 1024 streams).
-//   * stream bytes: per-lane ring of RSLOTS x 16 B in LDS, laid out
-//     [dword][lane] (bank = lane: conflict-free whatever each lane reads).
-//     Ring refills are wave-UNIFORM: every DTILE steps each lane writes the
-//     chunks it loaded DTILE steps earlier (register staged, so the global
-//     load latency overlaps a whole tile) and issues loads for up to two more.
-//     A lane only ever reads its own ring column, so no barrier is needed.
-//   * window: 64-bit MSB-first bit window. A step consumes at most 16 bits
-//     (x >= 16 after a decode), so one 32-bit refill per PAIR of steps keeps
-//     it >= 32 bits at every pair start; the next dword is prefetched from the
-//     ring one pair ahead.
-//   * output: step k of stream s is byte k*N + s, so at every step a wave
-//     stores 64 consecutive bytes (one coalesced byte-store instruction, row
-//     base in SGPRs, no VALU work).
+// xN decode, one 1024-lane workgroup per CU (the 2^18 streams of the
+// 256 MiB workload are exactly 1024 per CU). One lane = one stream.
+//   * LDS: the packed slot table at offset 0 (16 KiB) and a per-lane ring of
+//     the stream bytes, 32 dword rows x 1024 lanes ([row][lane]: bank = lane)
+//     plus a mirror of row 0 at row 32, 148 KiB in all. Stream byte A lives
+//     in row ((A >> 2) + 1) & 31, so the dword pair holding bytes
+//     [p-4, p) starts at row (p >> 2) & 31: one ds_read2st64 + v_alignbit.
+//   * renormalisation (rans.rs:479-485) without a bit window: with
+//     c = clz(x) and s = c & 24 (8 + 8 * bytes needed), the 64-bit shift
+//     (x : D) << s leaves x_renorm << 8 in the high dword, so the slot
+//     address and x >> 12 come straight out of it, and the low dword, one
+//     byte realigned, is the window of the second step of the pair.
+//   * one ring read per PAIR of steps: a step consumes at most 2 bytes, so
+//     the 4 bytes below the pair's start position cover both steps.
+//   * refills: every DT2 steps a lane whose unread bytes fall to 64 loads
+//     the next 64-B segment into registers; the segment is written into
+//     the ring two tile boundaries later, so loads have 2*DT2 steps to land.
+//     The wave waits with an exact vmcnt (stores and loads in between).
+//   * a lane whose reads outrun its ring (more than ~1.3 bytes per symbol
+//     sustained, only possible for data far from its table) sets the
+//     workgroup's redo flags: k_dec_xn<true> decodes those streams again.
+//   * output: step k of stream s is raw[k*N + s]: per step one buffer byte
+//     store per wave, row offset in an SGPR, no VALU address work.
 // ----------------------------------------------------------------------
-constexpr int FW = 512;
-constexpr int RSLOTS = 8;
-constexpr int DTILE = 16;
+constexpr int FW2 = 1024;
+constexpr int RR = 32;   // ring rows (dwords) per lane
+constexpr int DT2 = 16;  // steps per tile
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
+    // the base is wave-uniform; say so, or the compiler may keep the descriptor
+    // in VGPRs and wrap every store in a readfirstlane loop
+    const uint64_t p = (uint64_t)base;
+    // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(u), 0, 0x7FFFFFFF, 0x00020000);
+}
 
-__global__ __launch_bounds__(FW) void k_dec_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
-                                                 uint32_t nblkF) {
+// ABL: diagnostic ablations for profiling only (1: no output stores, 2: no slot
+// table read, 4: no ring refills, 8: per-workgroup timeline records written to
+// the workspace scratch area); the product path instantiates ABL = 0.
+template <int ABL>
+__global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
+                                                uint32_t nblkF) {
     const uint32_t b = blockIdx.x / nblkF, blkF = blockIdx.x % nblkF;
+    const uint64_t dbg_t0 = (ABL & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t dbg_c0 = (ABL & 8) ? __builtin_amdgcn_s_memtime() : 0;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
     if (n == 0 || single_mode(n, N) || a.status[b] != 0) return;
-    constexpr uint32_t RD = RSLOTS * 4;  // ring dwords per lane
-    __shared__ uint32_t stab[TOTFREQ];
-    __shared__ __attribute__((aligned(16))) uint32_t ringw[RD * FW];  // [dword][lane]
-    // scan scratch and flag alias the ring (used before it is filled): keeps the
-    // workgroup at exactly 80 KiB of LDS so two fit on a CU
-    unsigned long long *sh = reinterpret_cast<unsigned long long *>(ringw);
-    uint32_t *flag = ringw + 64;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[TOTFREQ + (RR + 1) * FW2];
+    uint32_t *ring = lds + TOTFREQ;
+    // scan scratch and flag alias the ring (used before it is filled)
+    unsigned long long *sh = reinterpret_cast<unsigned long long *>(ring);
+    uint32_t *flag = ring + 64;
     const uint32_t tid = threadIdx.x;
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
-    for (uint32_t j = tid; j < TOTFREQ; j += FW) stab[j] = T->slot[j];
+    {
+        const v4u *src = reinterpret_cast<const v4u *>(T->slot);
+        v4u *dst = reinterpret_cast<v4u *>(lds);
+        dst[tid] = src[tid];
+    }
     const uint32_t kind = T->kind;
-    const uint32_t s = blkF * FW + tid;
+    const uint32_t s = blkF * FW2 + tid;
     const bool active = s < N;
     const uint8_t *e = enc + a.enc_off[b];
     const uint32_t L = active ? ld_u32_u(e + 8 * (size_t)N + 4 * (size_t)s) : 0;
-    // 512-lane exclusive scan of the stream lengths + base of the first 256-block
-    unsigned long long inc = wave_incl_scan(L);
+    const unsigned long long inc = wave_incl_scan(L);
     const int wv = tid >> 6;
     if ((tid & 63) == 63) sh[wv] = inc;
     if (tid == 0) *flag = 0;
     __syncthreads();
     unsigned long long base = 0;
     for (int i = 0; i < wv; i++) base += sh[i];
-    const uint64_t off = base + inc - L + w.blockoff[(size_t)b * w.nblk + 2 * blkF];
+    const uint32_t nblk = w.nblk;
+    const uint64_t off = base + inc - L + w.blockoff[(size_t)b * nblk + 4 * blkF];
     const uint64_t X = active ? ld_u64_u(e + 8 * (size_t)s) : RANS_L;
-    uint8_t *outb = raw + a.raw_off[b];
     const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24);
     if (!fast) atomicOr(flag, 1u);
     __syncthreads();
     const uint32_t any_slow = *flag;
     __syncthreads();  // scan/flag reads complete before the ring is written
+    auto mark_redo = [&]() {
+        for (uint32_t i = 0; i < 4; i++)
+            if (4 * blkF + i < nblk) w.redo[(size_t)b * nblk + 4 * blkF + i] = 1;
+    };
     if (any_slow) {
-        if (tid == 0) {
-            w.redo[(size_t)b * w.nblk + 2 * blkF] = 1;
-            if (2 * blkF + 1 < w.nblk) w.redo[(size_t)b * w.nblk + 2 * blkF + 1] = 1;
-        }
+        if (tid == 0) mark_redo();
         return;
     }
     const uint64_t c = active ? (n - s - 1) / N + 1 : 0;
     const uint64_t cmax = (n - 1) / N + 1;
-    const uintptr_t sb = (uintptr_t)e + 12 * (size_t)N + off;  // stream start
-    const uintptr_t lo_lim = ((uintptr_t)e) & ~(uintptr_t)15;     // safe lower bound for loads
-    uint32_t *ring = ringw + tid;
-    // byte address -> this lane's ring dword (the dword holding that address)
-    auto rdw = [&](uint32_t addr) -> uint32_t { return ring[((addr >> 2) & (RD - 1)) * FW]; };
-    auto put16 = [&](uint32_t addr, const v4u v) {  // chunk at 16-aligned addr
-        const uint32_t d = (addr >> 2) & (RD - 1);
-        ring[(d + 0) * FW] = v.x;
-        ring[(d + 1) * FW] = v.y;
-        ring[(d + 2) * FW] = v.z;
-        ring[(d + 3) * FW] = v.w;
-    };
-    auto clampa = [&](uintptr_t addr) -> uintptr_t { return addr > lo_lim ? addr : lo_lim; };
-    // ---- ring prologue (synchronous): the 64-B segment holding the stream's
-    // last byte, and the segment below it. Later refills move whole 64-B
-    // segments (4 chunks issued back to back), so each L2 line is requested
-    // in one burst instead of chunk by chunk across tiles.
+    const uintptr_t sb = (uintptr_t)e + 12 * (size_t)N + off;
     const uintptr_t pend = sb + L;
-    const uintptr_t top = ((pend - 1) & ~(uintptr_t)15) + 16;  // end of the last chunk
-    uintptr_t lo = (top - 1) & ~(uintptr_t)63;                   // lowest byte loaded or in flight
-    {
-        for (uintptr_t cpos = top - 16; cpos + 1 > lo; cpos -= 16)
-            put16((uint32_t)cpos, *reinterpret_cast<const v4u *>(clampa(cpos)));
-        const uintptr_t g = lo - 64;
-        const v4u c0 = *reinterpret_cast<const v4u *>(clampa(g + 48));
-        const v4u c1 = *reinterpret_cast<const v4u *>(clampa(g + 32));
-        const v4u c2 = *reinterpret_cast<const v4u *>(clampa(g + 16));
-        const v4u c3 = *reinterpret_cast<const v4u *>(clampa(g));
-        put16((uint32_t)(g + 48), c0);
-        put16((uint32_t)(g + 32), c1);
-        put16((uint32_t)(g + 16), c2);
-        put16((uint32_t)g, c3);
-        lo = g;
-    }
-    // window: the dword holding the last stream byte, its garbage top bytes shifted out
-    const uintptr_t a0 = (pend - 1) & ~(uintptr_t)3;
-    const uint32_t v0 = (uint32_t)(pend - a0);
-    uint32_t x = (uint32_t)X;
-    uint64_t win = (uint64_t)(rdw((uint32_t)a0) << (32 - 8 * v0)) << 32;
-    uint32_t nbits = 8 * v0;
-    const uint32_t pend32 = (uint32_t)pend;
-    uint32_t cons = (uint32_t)a0;  // (low 32 bits) bytes [cons, pend) have entered the window
-    uint32_t nextw = rdw(cons - 4);
-    // a staged segment in flight. Inline asm so hipcc inserts no conservative
-    // vmcnt(0) (it would also wait for the tile's stores); the boundary below
-    // waits with an exact count instead.
-    v4u st0 = {0, 0, 0, 0}, st1 = st0, st2 = st0, st3 = st0;
-    bool pending = false;
-    uint32_t stlo = 0;
-    const bool wave_live = (uint64_t)blkF * FW + (tid & ~63u) < N;  // wave-uniform
-
-    // one 32-bit refill (branchless), then prefetch the next ring dword
-    auto refill = [&]() {
-        const bool need = nbits <= 32;
-        win |= (uint64_t)(need ? nextw : 0u) << ((32 - nbits) & 63);
-        nbits += need ? 32u : 0u;
-        cons -= need ? 4u : 0u;
-        nextw = rdw(cons - 4);
+    const uintptr_t lo_lim = ((uintptr_t)e) & ~(uintptr_t)63;
+    auto clampa = [&](uintptr_t p) -> uintptr_t { return p > lo_lim ? p : lo_lim; };
+    uint32_t *lring = ring + tid;
+    // write the 64-B segment at absolute address g (64-aligned; cK = bytes g+16K..)
+    auto put_seg = [&](uint32_t g, const v4u c0, const v4u c1, const v4u c2, const v4u c3) {
+        const uint32_t r0 = ((g >> 2) + 1) & (RR - 1);  // 1 or 17
+        uint32_t *p = lring + r0 * FW2;
+        p[0 * FW2] = c0.x; p[1 * FW2] = c0.y; p[2 * FW2] = c0.z; p[3 * FW2] = c0.w;
+        p[4 * FW2] = c1.x; p[5 * FW2] = c1.y; p[6 * FW2] = c1.z; p[7 * FW2] = c1.w;
+        p[8 * FW2] = c2.x; p[9 * FW2] = c2.y; p[10 * FW2] = c2.z; p[11 * FW2] = c2.w;
+        p[12 * FW2] = c3.x; p[13 * FW2] = c3.y; p[14 * FW2] = c3.z;
+        p[15 * FW2] = c3.w;                      // row 16, or the mirror row 32
+        if (r0 != 1) lring[0] = c3.w;            // row 0 itself
     };
-    refill();  // >= 32 bits before the first pair
-    uint32_t cons_snap = cons;
-    uint32_t nbits_snap = nbits;
-    // one decode step: renormalise (rans.rs:479-485) then decode (rans.rs:488-504);
-    // returns the slot entry (its low byte is the symbol)
-    auto step = [&]() -> uint32_t {
-        // x in [16, 2^24) needs 0, 1 or 2 bytes; the shift is 8 * #bytes
-        const uint32_t sh8 = (__builtin_clz(x) & 24) - 8;
-        x = (uint32_t)(((((uint64_t)x) << 32) | (uint32_t)(win >> 32)) << sh8 >> 32);
-        win <<= sh8;
-        nbits -= sh8;
-        const uint32_t ent = stab[x & (TOTFREQ - 1)];
-        x = __umul24(ent >> 20, x >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
+    // prologue: the 64-B segment holding the last stream byte and the one below
+    const uintptr_t g1 = (pend - 1) & ~(uintptr_t)63;
+    {
+        const v4u *p1 = reinterpret_cast<const v4u *>(clampa(g1));
+        const v4u *p0 = reinterpret_cast<const v4u *>(clampa(g1 - 64));
+        const v4u a0 = p1[0], a1 = p1[1], a2 = p1[2], a3 = p1[3];
+        const v4u b0 = p0[0], b1 = p0[1], b2 = p0[2], b3 = p0[3];
+        put_seg((uint32_t)g1, a0, a1, a2, a3);
+        put_seg((uint32_t)(g1 - 64), b0, b1, b2, b3);
+    }
+    // positions are tracked as byte address * 8 (mod 2^32): the ring only needs the
+    // low bits and comparisons use 32-bit differences
+    uintptr_t lo64 = g1 - 64;            // lowest resident byte (absolute)
+    uint32_t pos8 = (uint32_t)pend << 3;  // bytes [.., pos) not yet consumed
+    uint32_t x = (uint32_t)X;
+    // D: the 4 stream bytes below p (byte p-1 on top)
+    auto readD = [&](uint32_t p8) -> uint32_t {
+        const uint32_t *q = lring + ((p8 >> 5) & (RR - 1)) * FW2;
+        return __builtin_amdgcn_alignbit(q[FW2], q[0], p8);
+    };
+    // one decode step (rans.rs:472-507): renormalise from window D, decode, return
+    // the slot entry; hi/lo are the shifted (x : D) pair, sft = 8 + 8 * bytes consumed
+    auto step = [&](uint32_t D, uint32_t &hi, uint32_t &lo, uint32_t &sft) -> uint32_t {
+        sft = __builtin_clz(x) & 24;
+        const uint64_t t = ((((uint64_t)x) << 32) | D) << sft;
+        hi = (uint32_t)(t >> 32);
+        lo = (uint32_t)t;
+        const uint32_t ent = (ABL & 2) ? (hi & 0x0FFFFF00u) | 0x01000000u
+                                       : *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) +
+                                                                             ((hi >> 6) & 0x3FFC));
+        x = __umul24(ent >> 20, hi >> 20) + ((ent >> 8) & 0xFFF);
         return ent;
     };
-    // output: at step k the wave's lanes write bytes k*N + s .. +63 -- one
-    // coalesced 64-byte byte-store per wave per step, row base in SGPRs
-    const bool wave_all = (uint64_t)blkF * FW + (tid & ~63u) + 64 <= N;  // wave-uniform
+    uint32_t sink = 0;
+    // staging registers of the segment loads issued at even / odd boundaries
+    v4u e0 = {0, 0, 0, 0}, e1 = e0, e2 = e0, e3 = e0, o0 = e0, o1 = e0, o2 = e0, o3 = e0;
+    bool pnd = false;  // this lane has a segment in flight
+    uint32_t ptile = 0;
+    bool bad = false;
+    const uint64_t wbase = (uint64_t)blkF * FW2 + (tid & ~63u);
+    const bool wave_live = wbase < N;       // wave-uniform
+    const bool wave_all = wbase + 64 <= N;  // wave-uniform
+    uint8_t *outb = raw + a.raw_off[b] + (size_t)blkF * FW2;
+    // output rows are addressed through a descriptor rebased every tile, so the
+    // 32-bit buffer offsets cover any buffer size
+    __amdgpu_buffer_rsrc_t orsrc = byte_rsrc(outb);
+    const uint32_t nfull = (uint32_t)((cmax - 1) / DT2);  // tiles with k0 + DT2 < cmax
+    auto lov8 = [&]() -> uint32_t { return (uint32_t)lo64 << 3; };
+    // lanes that fetch nothing at a boundary load a line of the table instead
+    // (L2-resident, one request per wave): the loads are issued unconditionally
+    // so that no control flow ever merges a staging register still in flight
+    const uintptr_t dummy = (uintptr_t)T->slot + 64 * (tid >> 6);
 
-    bool prev_full = true;
-    for (uint64_t k0 = 0; k0 < cmax; k0 += DTILE) {
-        // ---- ring maintenance (wave-uniform position, per-lane masks)
-        if (k0 > 0) {
-            // the previous boundary's segment loads are followed by exactly DTILE
-            // byte stores of this wave when that tile was full and the wave is live
-            if (prev_full && wave_live)
-                asm volatile("s_waitcnt vmcnt(16)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
+    // tile boundary t, staging set (s0..s3) = the set of parity t & 1
+    auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3) {
+        // every read of the previous tile was at or above pos - 4
+        bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        if (t >= 2) {
+            // wait for the loads of boundary t-2: younger are the 16 stores of tile
+            // t-2, the 4 loads of boundary t-1 and the 16 stores of tile t-1
+            if ((ABL & 1) && wave_all)
+                asm volatile("s_waitcnt vmcnt(4)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
+            else if (wave_all)
+                asm volatile("s_waitcnt vmcnt(36)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
             else
-                asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
-            if (pending) {
-                put16(stlo + 48, st0);
-                put16(stlo + 32, st1);
-                put16(stlo + 16, st2);
-                put16(stlo, st3);
-            }
-            // <= 4 chunks still unread: the next 64-B segment fits the 8-chunk ring
-            const uint32_t occ = ((cons - 1 - (uint32_t)lo) >> 4) + 1;
-            pending = occ <= 4;
-            if (pending) {
-                asm_load16(st0, clampa(lo - 16));
-                asm_load16(st1, clampa(lo - 32));
-                asm_load16(st2, clampa(lo - 48));
-                asm_load16(st3, clampa(lo - 64));
-                lo -= 64;
-                stlo = (uint32_t)lo;
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
+            if (pnd && ptile + 2 == t) {
+                lo64 -= 64;
+                put_seg((uint32_t)lo64, s0, s1, s2, s3);
+                pnd = false;
             }
         }
-        const bool full = k0 + DTILE < cmax;  // every row of the tile is complete for every stream
-        if (full && wave_all) {
+        // a lane with <= 64 unread resident bytes fetches the segment below
+        const bool issue = !(ABL & 4) && active && !pnd && (int32_t)(pos8 - lov8()) <= 64 * 8;
+        const uintptr_t g = issue ? clampa(lo64 - 64) : dummy;
+        asm_load16(s0, g);
+        asm_load16(s1, g + 16);
+        asm_load16(s2, g + 32);
+        asm_load16(s3, g + 48);
+        if (issue) {
+            pnd = true;
+            ptile = t;
+        }
+    };
+    // DT2 steps in pairs; one ring read per pair
+    auto tile = [&](uint32_t t) {
+        uint32_t D = readD(pos8);
+        orsrc = byte_rsrc(outb + (uint64_t)t * DT2 * N);
+        uint32_t row = 0;
 #pragma unroll
-            for (int j = 0; j < DTILE; j++) {
-                const uint32_t ent = step();
-                if (j & 1) refill();
-                (outb + (k0 + j) * N)[s] = (uint8_t)ent;
+        for (int j = 0; j < DT2 / 2; j++) {
+            uint32_t hA, lA, sA, hB, lB, sB;
+            const uint32_t eA = step(D, hA, lA, sA);
+            const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
+            pos8 = pos8 + 16 - sA - sB;
+            if (j + 1 < DT2 / 2) D = readD(pos8);
+            if (ABL & 1) {
+                sink += eA ^ eB;
+            } else if (wave_all || active) {
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, tid, row, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eB, orsrc, tid, row + N, 0);
             }
-        } else if (full) {
-#pragma unroll
-            for (int j = 0; j < DTILE; j++) {
-                const uint32_t ent = step();
-                if (j & 1) refill();
-                if (active) (outb + (k0 + j) * N)[s] = (uint8_t)ent;
-            }
-        } else {
-            const uint32_t nsteps = (uint32_t)(cmax - k0);
-            for (uint32_t j = 0; j < nsteps; j++) {
-                const uint64_t k = k0 + j;
-                if (k == c) {  // first step past this lane's symbols
-                    cons_snap = cons;
-                    nbits_snap = nbits;
-                }
-                const uint32_t ent = step();
-                if (j & 1) refill();
-                if (k < c) (outb + k * N)[s] = (uint8_t)ent;
+            row += 2 * N;
+        }
+    };
+
+    if (wave_live) {
+        for (uint32_t t = 0; t < nfull; t += 2) {
+            boundary(t, e0, e1, e2, e3);
+            tile(t);
+            if (t + 1 < nfull) {
+                boundary(t + 1, o0, o1, o2, o3);
+                tile(t + 1);
             }
         }
-        prev_full = full;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(st0), "+v"(st1), "+v"(st2), "+v"(st3)::"memory");
-    if (c == cmax) {  // no step past the end was executed for this lane
-        cons_snap = cons;
-        nbits_snap = nbits;
-    }
-    // bytes consumed by renormalisation = bytes moved into the window - bits still there
-    if (active) {
-        const uint64_t consumed = (uint64_t)(pend32 - cons_snap) - nbits_snap / 8;
-        if (consumed > L) a.status[b] = ZR_INVALID_INPUT;  // "Insufficient data" (rans.rs:480-482)
+        // ---- last tile (1..DT2 steps): every segment in flight lands first
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
+                     "+v"(o2), "+v"(o3)::"memory");
+        bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        if (pnd) {
+            lo64 -= 64;
+            if (ptile & 1)
+                put_seg((uint32_t)lo64, o0, o1, o2, o3);
+            else
+                put_seg((uint32_t)lo64, e0, e1, e2, e3);
+        }
+        uint32_t pos_snap = pos8;
+        const uint64_t k0 = (uint64_t)nfull * DT2;
+        const uint32_t nst = (uint32_t)(cmax - k0);
+        orsrc = byte_rsrc(outb + k0 * N);
+        for (uint32_t j = 0; j < nst; j++) {
+            const uint64_t k = k0 + j;
+            const bool live = k < c;
+            if (live) bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
+            uint32_t h, l, sf;
+            const uint32_t ent = step(readD(pos8), h, l, sf);
+            pos8 = pos8 + 8 - sf;
+            if (live) {
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ent, orsrc, tid, (uint32_t)(j * N), 0);
+                pos_snap = pos8;
+            }
+        }
+        if ((ABL & 1) && sink == 0x9E3779B9u) a.status[b] = 7;  // keeps the ablated work live
+        if ((ABL & 8) && tid == 0) {
+            uint64_t *r = reinterpret_cast<uint64_t *>(w.scratch) + 4 * (size_t)blockIdx.x;
+            r[0] = dbg_t0;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+            r[2] = __builtin_amdgcn_s_memtime() - dbg_c0;
+            r[3] = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) | ((uint64_t)__builtin_amdgcn_s_getreg(0xF814) << 32);
+        }
+        if (active) {
+            if (bad) {
+                mark_redo();
+            } else {
+                // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
+                const uint32_t consumed = (((uint32_t)pend << 3) - pos_snap) >> 3;
+                if (consumed > L) a.status[b] = ZR_INVALID_INPUT;
+            }
+        }
     }
 }
 
@@ -1402,8 +1457,20 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
         hipLaunchKernelGGL(k_dec_hdr, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
         hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
         timer_begin("rans_decode", s);
-        const uint32_t nblkF = (uint32_t)ceil_div(a.N, FW);
-        hipLaunchKernelGGL(k_dec_fast, dim3(nblkF * a.B), dim3(FW), 0, s, enc, raw, a, w, nblkF);
+        if (a.N >= (1u << 27))  // a tile of DT2 output rows must span < 2^31 bytes
+            return set_error(ZR_UNSUPPORTED, "more than 2^27 rANS streams");
+        const uint32_t nblkF = (uint32_t)ceil_div(a.N, FW2);
+        static const int abl = getenv("ZR_DEC_ABL") ? atoi(getenv("ZR_DEC_ABL")) : 0;  // profiling only
+        auto kern = k_dec_xn_fast<0>;
+        switch (abl) {
+            case 1: kern = k_dec_xn_fast<1>; break;
+            case 2: kern = k_dec_xn_fast<2>; break;
+            case 4: kern = k_dec_xn_fast<4>; break;
+            case 7: kern = k_dec_xn_fast<7>; break;
+            case 8: kern = k_dec_xn_fast<8>; break;
+            default: break;
+        }
+        hipLaunchKernelGGL(kern, dim3(nblkF * a.B), dim3(FW2), 0, s, enc, raw, a, w, nblkF);
         timer_end("rans_decode", s);
         hipLaunchKernelGGL(k_dec_xn<true>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
     }
