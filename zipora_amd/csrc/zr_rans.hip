@@ -19,6 +19,7 @@
 namespace zr {
 
 // ------------------------------------------------------------------ helpers
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t ld_u32_u(const uint8_t *p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
@@ -82,55 +83,85 @@ struct KArgs {  // kernel-side copy of zr_rans_batch
 // histogram (the callers' [u32;256] counts: compression/mod.rs:433-436,
 // blob_store/entropy.rs:213-216, rans.rs:708-714)
 // ======================================================================
-__device__ __forceinline__ void hist_range(const uint8_t *p, uint64_t lo, uint64_t hi, uint32_t *mine) {
+// LDS histogram with 32 bank-spread copies: lane l counts into copy l & 31 at
+// h[bin * 32 + copy], so the 32 lanes of a half-wave always hit 32 distinct
+// banks and never the same address, whatever the bytes are.
+constexpr int HCOPY = 32;
+__device__ __forceinline__ void hist_add4(uint32_t *h, uint32_t w, uint32_t cp) {
+    atomicAdd(&h[((w & 0xFF) << 5) + cp], 1u);
+    atomicAdd(&h[(((w >> 8) & 0xFF) << 5) + cp], 1u);
+    atomicAdd(&h[(((w >> 16) & 0xFF) << 5) + cp], 1u);
+    atomicAdd(&h[((w >> 24) << 5) + cp], 1u);
+}
+
+// Count bytes [lo, hi) of p into h with T threads (T = 64: one wave, T = 256:
+// the workgroup); tid in [0, T).
+template <uint32_t T>
+__device__ __forceinline__ void hist_range(const uint8_t *p, uint64_t lo, uint64_t hi, uint32_t *h,
+                                           uint32_t tid) {
+    const uint32_t cp = threadIdx.x & (HCOPY - 1);
     // head bytes up to 16-byte alignment
     const uint64_t mis = (16 - (((uintptr_t)(p + lo)) & 15)) & 15;
     const uint64_t body_lo = min(hi, lo + mis);
-    if (threadIdx.x < body_lo - lo) atomicAdd(&mine[p[lo + threadIdx.x]], 1u);
+    if (tid < body_lo - lo) atomicAdd(&h[((uint32_t)p[lo + tid] << 5) + cp], 1u);
     const uint64_t units = (hi - body_lo) / 16;
-    const uint4 *q = reinterpret_cast<const uint4 *>(p + body_lo);
-    for (uint64_t u = threadIdx.x; u < units; u += 256) {
-        uint4 v = q[u];
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            atomicAdd(&mine[w[j] & 0xFF], 1u);
-            atomicAdd(&mine[(w[j] >> 8) & 0xFF], 1u);
-            atomicAdd(&mine[(w[j] >> 16) & 0xFF], 1u);
-            atomicAdd(&mine[w[j] >> 24], 1u);
-        }
+    const v4u *q = reinterpret_cast<const v4u *>(p + body_lo);
+    uint64_t u = tid;
+    // four 16-byte loads in flight per thread
+    for (; u + 3 * T < units; u += 4 * T) {
+        const v4u v0 = __builtin_nontemporal_load(q + u);
+        const v4u v1 = __builtin_nontemporal_load(q + u + T);
+        const v4u v2 = __builtin_nontemporal_load(q + u + 2 * T);
+        const v4u v3 = __builtin_nontemporal_load(q + u + 3 * T);
+        hist_add4(h, v0.x, cp); hist_add4(h, v0.y, cp); hist_add4(h, v0.z, cp); hist_add4(h, v0.w, cp);
+        hist_add4(h, v1.x, cp); hist_add4(h, v1.y, cp); hist_add4(h, v1.z, cp); hist_add4(h, v1.w, cp);
+        hist_add4(h, v2.x, cp); hist_add4(h, v2.y, cp); hist_add4(h, v2.z, cp); hist_add4(h, v2.w, cp);
+        hist_add4(h, v3.x, cp); hist_add4(h, v3.y, cp); hist_add4(h, v3.z, cp); hist_add4(h, v3.w, cp);
+    }
+    for (; u < units; u += T) {
+        const v4u v = q[u];
+        hist_add4(h, v.x, cp); hist_add4(h, v.y, cp); hist_add4(h, v.z, cp); hist_add4(h, v.w, cp);
     }
     const uint64_t tail_lo = body_lo + units * 16;
-    if (threadIdx.x < hi - tail_lo) atomicAdd(&mine[p[tail_lo + threadIdx.x]], 1u);
+    if (tid < hi - tail_lo) atomicAdd(&h[((uint32_t)p[tail_lo + tid] << 5) + cp], 1u);
 }
 
-// Work item = (buffer, 64 KiB chunk). Per-buffer histograms: one workgroup
-// per item. Shared histogram: a grid-stride loop over the items with one LDS
-// histogram per workgroup and one global add per bin at the end (a batch of
-// a million 1 KiB records would otherwise send a global atomic per bin per
-// record to the same 256 counters).
+// Work item = (buffer, 64 KiB chunk).
+//  * per-buffer histograms: one workgroup per item, its LDS histogram added to
+//    the buffer's counts at the end;
+//  * shared histogram: every WAVE takes items (grid-stride over waves), so a
+//    batch of a million 1 KiB records keeps all 64 lanes of a wave busy, and
+//    each workgroup adds one LDS histogram to the 256 global counters at the
+//    end (a global atomic per bin per record would serialise on 256 words).
 __global__ __launch_bounds__(256) void k_hist(const uint8_t *raw, KArgs a, int shared,
                                               uint32_t *hist, uint64_t chunk, uint32_t nchunk) {
-    __shared__ uint32_t h[4][257];
-    for (int i = threadIdx.x; i < 4 * 257; i += 256) (&h[0][0])[i] = 0;
+    __shared__ uint32_t h[256 * HCOPY];
+    for (int i = threadIdx.x; i < 256 * HCOPY; i += 256) h[i] = 0;
     __syncthreads();
-    uint32_t *mine = h[threadIdx.x >> 6];
     const uint64_t items = (uint64_t)a.B * nchunk;
-    const uint64_t step = shared ? gridDim.x : items;
-    for (uint64_t it = blockIdx.x; it < items; it += step) {
-        const uint32_t b = (uint32_t)(it / nchunk), c = (uint32_t)(it % nchunk);
+    if (shared) {
+        const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (uint64_t it = (uint64_t)blockIdx.x * 4 + wv; it < items; it += (uint64_t)gridDim.x * 4) {
+            const uint32_t b = (uint32_t)(it / nchunk), c = (uint32_t)(it % nchunk);
+            const uint64_t n = a.len[b];
+            const uint64_t lo = (uint64_t)c * chunk;
+            if (lo < n) hist_range<64>(raw + a.raw_off[b], lo, min(n, lo + chunk), h, lane);
+        }
+    } else {
+        const uint32_t b = (uint32_t)(blockIdx.x / nchunk), c = (uint32_t)(blockIdx.x % nchunk);
         const uint64_t n = a.len[b];
         const uint64_t lo = (uint64_t)c * chunk;
-        if (lo >= n) continue;
-        hist_range(raw + a.raw_off[b], lo, min(n, lo + chunk), mine);
-        if (!shared) break;
+        if (lo < n) hist_range<256>(raw + a.raw_off[b], lo, min(n, lo + chunk), h, threadIdx.x);
     }
     __syncthreads();
+    // bin v = thread: sum its 32 copies, rotated so the threads hit distinct banks
     const uint32_t v = threadIdx.x;
-    const uint32_t s = h[0][v] + h[1][v] + h[2][v] + h[3][v];
-    if (s) {
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t k = 0; k < HCOPY; k++) sum += h[(v << 5) + ((k + v) & (HCOPY - 1))];
+    if (sum) {
         const uint32_t b = (uint32_t)(blockIdx.x / nchunk);
-        atomicAdd(&hist[(shared ? 0 : (size_t)b * 256) + v], s);
+        atomicAdd(&hist[(shared ? 0 : (size_t)b * 256) + v], sum);
     }
 }
 
@@ -226,7 +257,6 @@ __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tab
     }
 }
 
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void asm_load16(v4u &dst, uintptr_t addr) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(addr) : "memory");
 }
@@ -1380,7 +1410,8 @@ int32_t zr_histogram_dev(const uint8_t *raw, const zr_rans_batch *bt, int32_t sh
     const uint64_t chunk = 64 * 1024;
     const uint32_t nchunk = (uint32_t)ceil_div(bt->max_len, chunk);
     const uint64_t items = (uint64_t)nchunk * a.B;
-    const uint64_t grid = shared ? std::min<uint64_t>(items, 8192) : items;
+    // shared: 5 resident 32-KiB-LDS workgroups per CU on 256 CUs, 4 waves each
+    const uint64_t grid = shared ? std::min<uint64_t>(ceil_div(items, 4), 1280) : items;
     timer_begin("histogram", (hipStream_t)stream);
     hipLaunchKernelGGL(k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a,
                        shared, hist_dev, chunk, nchunk);
