@@ -111,6 +111,29 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *batch, const uint8_t *raw,
 int32_t zr_rans_decode_batch_dev(const zr_rans_batch *batch, const uint8_t *enc, uint8_t *raw,
                                  void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---- host-resident batches (blob-store records, file buffers) ----
+ * The same batch coding with every array in HOST memory: buffers are cut into
+ * groups of whole buffers (<= group_bytes raw bytes, 0 = 32 MiB) that stream
+ * through two device slots, so one group's host-to-device copy, the previous
+ * group's coding and the one before's copy back overlap. One shared table
+ * (the RansBlobStore / RansCompressor case: blob_store/entropy.rs:203-260,
+ * compression/mod.rs:433-470). Offsets are those of the device batch API;
+ * enc + enc_off[b] must hold zr_rans_encode_bound(len[b], n_streams) bytes on
+ * encode. Pin the host areas (zr_host_register) for the full PCIe rate. */
+typedef struct zr_rans_pipe zr_rans_pipe;
+int32_t zr_rans_pipe_create(const zr_rans_table *table, uint32_t n_streams, uint64_t group_bytes,
+                            zr_rans_pipe **out);
+int32_t zr_rans_pipe_destroy(zr_rans_pipe *pipe);
+int32_t zr_rans_pipe_encode(zr_rans_pipe *pipe, uint32_t n_buffers, const uint64_t *len,
+                            const uint8_t *raw, const uint64_t *raw_off, uint8_t *enc,
+                            const uint64_t *enc_off, uint64_t *enc_len, int32_t *status);
+int32_t zr_rans_pipe_decode(zr_rans_pipe *pipe, uint32_t n_buffers, const uint64_t *len,
+                            const uint8_t *enc, const uint64_t *enc_off, const uint64_t *enc_len,
+                            uint8_t *raw, const uint64_t *raw_off, int32_t *status);
+/* page-lock / unlock a host range for asynchronous copies */
+int32_t zr_host_register(void *ptr, size_t bytes);
+int32_t zr_host_unregister(void *ptr);
+
 /* ======================================================================
  * FSE (rANS with 32-bit renormalisation words) -- src/entropy/fse.rs
  * Stream formats (Appendix A): 0xF5 single | 0xF6 nblocks sizes bodies.

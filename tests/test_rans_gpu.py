@@ -179,3 +179,69 @@ def test_rans_full_size_property(zr, oracle):
         d = data[b * n:(b + 1) * n]
         t = oracle.rans_table(oracle.histogram(d))
         assert bt.encoded(enc, b) == oracle.rans_encode(t, N, d)
+
+
+def _pipe_roundtrip(zr, oracle, lens, N, kind, group_bytes, pinned=True):
+    """Host-resident batch through zr_rans_pipe_*: every buffer's bytes equal the
+    oracle's Rans64Encoder::encode under the shared table; decode restores the input."""
+    import numpy as np
+    import torch
+    from zipora_amd.device import RansHostPipe
+    datas = [zr.synth(kind, n, seed=3000 + b) for b, n in enumerate(lens)]
+    freqs = oracle.histogram(b"".join(datas))
+    table = zr.Rans64Encoder(freqs, N).table
+    pipe = RansHostPipe(table, N, group_bytes)
+    raw_off, enc_off, rb, eb = pipe.layout(lens)
+    raw = torch.zeros(max(rb, 1), dtype=torch.uint8, pin_memory=pinned)
+    for b, d in enumerate(datas):
+        o = int(raw_off[b])
+        raw[o:o + len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8) if d else raw[o:o]
+    enc = torch.zeros(max(eb, 1), dtype=torch.uint8, pin_memory=pinned)
+    enc_len, st = pipe.encode(lens, raw, raw_off, enc, enc_off)
+    assert (st == 0).all()
+    t = oracle.rans_table(freqs)
+    encb = enc.numpy()
+    for b, d in enumerate(datas):
+        o = int(enc_off[b])
+        assert encb[o:o + int(enc_len[b])].tobytes() == oracle.rans_encode(t, N, d), f"buffer {b}"
+    out = torch.zeros_like(raw)
+    st = pipe.decode(lens, enc, enc_off, enc_len, out, raw_off)
+    assert (st == 0).all()
+    outb = out.numpy()
+    for b, d in enumerate(datas):
+        o = int(raw_off[b])
+        assert outb[o:o + len(d)].tobytes() == d, f"buffer {b}"
+    pipe.close()
+
+
+def test_rans_host_pipe(zr, oracle):
+    # several groups per call (both slots reused), a buffer larger than a group,
+    # empty and tiny buffers, pageable memory
+    lens = [300000, 0, 5, 70000, 1 << 20, 4096, 200000, 123457, 1, 90000]
+    _pipe_roundtrip(zr, oracle, lens, 4096, "u", 256 << 10)
+    _pipe_roundtrip(zr, oracle, lens, 64, "t", 64 << 10, pinned=False)
+    _pipe_roundtrip(zr, oracle, [1024] * 200 + [17, 3], 1, "t", 32 << 10)
+    _pipe_roundtrip(zr, oracle, [], 4, "u", 1 << 20)
+
+
+def test_rans_host_pipe_errors(zr, oracle):
+    import numpy as np
+    import torch
+    from zipora_amd.device import RansHostPipe
+    freqs = oracle.histogram(b"aaaa")
+    pipe = RansHostPipe(zr.Rans64Encoder(freqs, 4).table, 4, 1 << 16)
+    lens = [100, 100]
+    raw_off, enc_off, rb, eb = pipe.layout(lens)
+    raw = torch.full((rb,), ord("a"), dtype=torch.uint8)
+    raw[150] = ord("b")  # symbol missing from the table: buffer 1 fails, buffer 0 codes
+    enc = torch.zeros(eb, dtype=torch.uint8)
+    enc_len, st = pipe.encode(lens, raw, raw_off, enc, enc_off)
+    assert st[0] == 0 and st[1] != 0
+    # truncated input: decode reports the buffer, the other one is restored
+    enc_len2 = enc_len.copy()
+    enc_len2[1] = 10
+    out = torch.zeros_like(raw)
+    enc_len2[0] = enc_len[0]
+    st = pipe.decode([100, 100], enc, enc_off, enc_len2, out, raw_off)
+    assert st[0] == 0 and st[1] != 0
+    assert bytes(out[:100].numpy()) == b"a" * 100

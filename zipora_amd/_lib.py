@@ -71,6 +71,15 @@ SIGNATURES = [
                                                   c_vp]),
     ("zr_rans_decode_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp, c_sz,
                                                   c_vp]),
+    ("zr_rans_pipe_create", ctypes.c_int32, [ctypes.POINTER(RansTable), ctypes.c_uint32, ctypes.c_uint64,
+                                             ctypes.POINTER(c_vp)]),
+    ("zr_rans_pipe_destroy", ctypes.c_int32, [c_vp]),
+    ("zr_rans_pipe_encode", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                             c_vp]),
+    ("zr_rans_pipe_decode", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                             c_vp]),
+    ("zr_host_register", ctypes.c_int32, [c_vp, c_sz]),
+    ("zr_host_unregister", ctypes.c_int32, [c_vp]),
     ("zr_fse_config_default", None, [ctypes.POINTER(FseConfig)]),
     ("zr_fse_compress_bound", c_sz, [c_sz, ctypes.POINTER(FseConfig)]),
     ("zr_fse_compress", ctypes.c_int32, [ctypes.POINTER(FseConfig), c_u8p, c_sz, c_u8p, c_sz,

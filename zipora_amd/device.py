@@ -123,3 +123,77 @@ class RansDeviceBatch:
     def raw_of(self, raw, b):
         off = self.raw_off_host[b]
         return bytes(raw[off: off + self.lens_host[b]].cpu().numpy().tobytes())
+
+
+class RansHostPipe:
+    """Host-resident rANS batches through the overlapped copy/code pipeline
+    (zr_rans_pipe_*): every array is host memory; one shared table.
+
+    The areas are uint8 CPU tensors (pinned ones reach the full PCIe rate);
+    offsets follow RansDeviceBatch's layout unless given.
+    """
+
+    def __init__(self, table, n_streams, group_bytes=32 << 20):
+        import numpy as np
+        self._np = np
+        self.L = _lib.load()
+        self.N = int(n_streams)
+        self._table = table
+        h = ctypes.c_void_p()
+        check(self.L.zr_rans_pipe_create(ctypes.byref(table), self.N, int(group_bytes), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            check(self.L.zr_rans_pipe_destroy(self.h))
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def layout(self, lens, align=16):
+        """(raw_off, enc_off, raw_bytes, enc_bytes) packing buffers back to back."""
+        np = self._np
+        lens = np.asarray(lens, dtype=np.uint64)
+        bound = np.array([self.L.zr_rans_encode_bound(int(n), self.N) for n in lens], dtype=np.uint64)
+        ra = (lens + align - 1) // align * align
+        ea = (bound + align - 1) // align * align
+        raw_off = np.concatenate([[0], np.cumsum(ra)[:-1]]).astype(np.uint64) if len(lens) else ra
+        enc_off = np.concatenate([[0], np.cumsum(ea)[:-1]]).astype(np.uint64) if len(lens) else ea
+        return raw_off, enc_off, int(ra.sum()), int(ea.sum())
+
+    @staticmethod
+    def _p(a):
+        if isinstance(a, torch.Tensor):
+            assert a.device.type == "cpu" and a.is_contiguous()
+            return ctypes.c_void_p(a.data_ptr())
+        return ctypes.c_void_p(a.ctypes.data)
+
+    def encode(self, lens, raw, raw_off, enc, enc_off):
+        """-> (enc_len, status) numpy arrays; raises on a call-level error."""
+        np = self._np
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        B = len(lens)
+        enc_len = np.zeros(B, dtype=np.uint64)
+        status = np.zeros(B, dtype=np.int32)
+        check(self.L.zr_rans_pipe_encode(self.h, B, self._p(lens), self._p(raw),
+                                         self._p(np.ascontiguousarray(raw_off, dtype=np.uint64)),
+                                         self._p(enc), self._p(np.ascontiguousarray(enc_off, dtype=np.uint64)),
+                                         self._p(enc_len), self._p(status)))
+        return enc_len, status
+
+    def decode(self, lens, enc, enc_off, enc_len, raw, raw_off):
+        """-> status numpy array."""
+        np = self._np
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        B = len(lens)
+        status = np.zeros(B, dtype=np.int32)
+        check(self.L.zr_rans_pipe_decode(self.h, B, self._p(lens), self._p(enc),
+                                         self._p(np.ascontiguousarray(enc_off, dtype=np.uint64)),
+                                         self._p(np.ascontiguousarray(enc_len, dtype=np.uint64)),
+                                         self._p(raw), self._p(np.ascontiguousarray(raw_off, dtype=np.uint64)),
+                                         self._p(status)))
+        return status
