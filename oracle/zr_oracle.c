@@ -759,7 +759,7 @@ static int copy_decode_tree(const btree *b, int node, or_huff_tree *t) {
 }
 
 /* insert_code_into_tree, tree.rs:359-469 (placeholder leaves: symbol 0, freq 0) */
-static uint8_t ph[1024]; /* placeholder flag per node (single-threaded oracle) */
+static _Thread_local uint8_t ph[1024]; /* placeholder flag per node (per thread: the CPU baseline runs threads) */
 static int insert_code(or_huff_tree *t, int node, uint8_t sym, uint64_t code, uint32_t len,
                        uint32_t at) {
     if (at == len) { /* empty code: replace node with a leaf */

@@ -583,7 +583,19 @@ __global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, Rans
         const uintptr_t ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
         const uint64_t nunits = ((uintptr_t)dbase + r1 - ua0 + 15) / 16;
         const uint64_t ulo = nunits * part / CSPLIT, uhi = nunits * (part + 1) / CSPLIT;
+        // first stream ending after this thread's first unit: binary search (a
+        // linear scan from stream 0 costs part*64 dependent LDS reads)
         uint32_t sj = 0;
+        {
+            const int64_t p = (int64_t)(ua0 + 16 * (ulo + threadIdx.x) - (uintptr_t)dbase);
+            uint32_t lo = 0, hi = nstream - 1;  // send_s[hi] > p or hi = last
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((int64_t)send_s[mid] <= p) lo = mid + 1;
+                else hi = mid;
+            }
+            sj = lo;
+        }
         for (uint64_t u = ulo + threadIdx.x; u < uhi; u += 256) {
             const uintptr_t ua = ua0 + 16 * u;
             // destination offset of the unit; negative for a first unit that starts in the header
@@ -650,6 +662,149 @@ __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, Ra
     if (threadIdx.x < 8) {
         const uint64_t x = w.st_state[(size_t)b * a.N];
         dst[L + threadIdx.x] = (uint8_t)(x >> (8 * threadIdx.x));
+    }
+}
+
+
+// Stream compaction through an LDS image of the destination (rans.rs:402-419):
+// a workgroup owns CS consecutive streams, whose bytes are contiguous in the
+// destination. Phase 1 reads each stream's scratch bytes with aligned 16-B
+// loads (a wave walks the flattened chunk list of its streams, CU_LD loads in
+// flight per lane) and writes them at their destination offsets into an LDS
+// window; phase 2 writes the window out with aligned 16-B stores. Only the
+// two edge units of the group, shared with the neighbouring groups, are
+// stored byte by byte. Windows repeat when a group's bytes exceed CWIN.
+template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD>  // streams per workgroup (divides 256), LDS window bytes, loads in flight per lane
+__global__ __launch_bounds__(256) void k_enc_compact_lds(uint8_t *enc, KArgs a, RansWork w) {
+    const uint32_t nblk = w.nblk;
+    const uint32_t gpb = 256 / CS;  // groups per 256-stream block
+    const uint32_t ngrp = nblk * gpb;
+    const uint32_t b = blockIdx.x / ngrp, grp = blockIdx.x % ngrp;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    const uint32_t N = a.N;
+    if (single_mode(n, N) || a.status[b] != 0) return;
+    const uint32_t blk = grp / gpb, s0 = grp * CS;
+    if (s0 >= N) return;
+    const uint32_t ns = min(CS, N - s0);
+    __shared__ unsigned long long sh[4];
+    __shared__ uint64_t soff[CS];
+    __shared__ uint32_t slen[CS], cpre[CS + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
+    const uint32_t tid = threadIdx.x;
+    {
+        // offsets of the block's streams (block scan), keep this group's
+        const uint32_t sb = blk * 256 + tid;
+        const uint32_t i = sb - s0;
+        const bool mine = sb >= s0 && i < ns;
+        const uint64_t bo = w.blockoff[(size_t)b * nblk + blk];
+        const uint32_t L = sb < N ? w.st_len[(size_t)b * N + sb] : 0;
+        const uint32_t X = mine ? w.st_state[(size_t)b * N + sb] : 0;
+        const uint64_t off = block_excl_scan(L, sh, nullptr) + bo;
+        if (mine) {
+            soff[i] = off;
+            slen[i] = L;
+            uint8_t *e = enc + a.enc_off[b];
+            if ((((uintptr_t)e) & 7) == 0) {
+                *reinterpret_cast<uint2 *>(e + 8 * (size_t)sb) = make_uint2(X, 0);
+                *reinterpret_cast<uint32_t *>(e + 8 * (size_t)N + 4 * (size_t)sb) = L;
+            } else {
+                st_u32_u(e + 8 * (size_t)sb, X);
+                st_u32_u(e + 8 * (size_t)sb + 4, 0);
+                st_u32_u(e + 8 * (size_t)N + 4 * (size_t)sb, L);
+            }
+        }
+        // chunk-count prefix (16-B source chunks per stream): the group's
+        // streams are lanes i of the waves holding them; CS <= 64 and groups
+        // are aligned, so one wave holds them all
+        const uint32_t cc = mine ? (L + 15) >> 4 : 0;
+        uint32_t inc = cc;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(inc, d, 64);
+            if ((tid & 63) >= d) inc += t;
+        }
+        // the wave's lanes below the group contribute 0 only if the group
+        // starts at lane 0 of the wave or lanes below are not mine (true: cc = 0)
+        if (mine) cpre[i + 1] = inc;
+        if (mine && i == 0) cpre[0] = 0;
+    }
+    __syncthreads();
+    uint8_t *dbase = enc + a.enc_off[b] + 12 * (size_t)N;
+    const uint64_t r0 = soff[0], r1 = soff[ns - 1] + slen[ns - 1];
+    if (r1 <= r0) return;
+    const uintptr_t ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
+    const uint64_t span = (uintptr_t)dbase + r1 - ua0;  // bytes of the image from ua0
+    const uint32_t nchunks = cpre[ns];
+    const uint8_t *sbase = w.scratch + (size_t)b * w.region + (size_t)s0 * w.cap;
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    for (uint64_t win = 0; win < span; win += CWIN) {
+        const uint64_t wend = min(span, win + (uint64_t)CWIN);
+        // ---- phase 1: chunks -> LDS image. Chunk f (flat index over the group)
+        // belongs to stream i with cpre[i] <= f < cpre[i+1].
+        uint32_t si = 0;
+        for (uint32_t f0 = wv * 64 * CU_LD; f0 < nchunks; f0 += 256 * CU_LD) {
+            v4u v[CU_LD];
+            int64_t dpos[CU_LD];  // image position of the chunk's first byte (relative to win)
+            uint32_t nv[CU_LD];   // valid bytes of the chunk
+            for (uint32_t k = 0; k < CU_LD; k++) {
+                const uint32_t f = f0 + 64 * k + lane;
+                nv[k] = 0;
+                dpos[k] = 0;
+                const uint8_t *src = sbase;
+                if (f < nchunks) {
+                    while (cpre[si + 1] <= f) si++;
+                    const uint32_t c = f - cpre[si];
+                    src = sbase + (size_t)si * w.cap + 16 * (size_t)c;
+                    nv[k] = min(16u, slen[si] - 16 * c);
+                    dpos[k] = (int64_t)((uintptr_t)dbase + soff[si] + 16 * (uint64_t)c - ua0) - (int64_t)win;
+                    if (dpos[k] + 16 <= 0 || dpos[k] >= (int64_t)(wend - win)) nv[k] = 0;  // not in this window
+                }
+                v[k] = *reinterpret_cast<const v4u *>(nv[k] ? src : sbase);
+            }
+            for (uint32_t k = 0; k < CU_LD; k++) {
+                if (!nv[k]) continue;
+                const int64_t p = dpos[k];
+                const uint32_t wl = (uint32_t)(wend - win);
+                if (nv[k] == 16 && p >= 0 && p + 16 <= (int64_t)wl && (p & 3) == 0) {
+                    uint32_t *d = reinterpret_cast<uint32_t *>(img + p);
+                    d[0] = v[k].x;
+                    d[1] = v[k].y;
+                    d[2] = v[k].z;
+                    d[3] = v[k].w;
+                } else if (nv[k] == 16 && p >= 0 && p + 20 <= (int64_t)wl) {
+                    // misaligned by a = p & 3: (4 - a) head bytes, 3 whole dwords, a tail bytes
+                    const uint32_t al = (uint32_t)p & 3, sh8 = 8 * (4 - al);
+                    const uint32_t w0 = v[k].x, w1 = v[k].y, w2 = v[k].z, w3 = v[k].w;
+                    for (uint32_t t = 0; t < 4 - al; t++) img[p + t] = (uint8_t)(w0 >> (8 * t));
+                    uint32_t *d = reinterpret_cast<uint32_t *>(img + p + 4 - al);
+                    d[0] = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh8);
+                    d[1] = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh8);
+                    d[2] = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh8);
+                    for (uint32_t t = 0; t < al; t++) img[p + 16 - al + t] = (uint8_t)(w3 >> (8 * (4 - al + t)));
+                } else {
+                    const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                    for (uint32_t t = 0; t < nv[k]; t++) {
+                        const int64_t q = p + t;
+                        if (q >= 0 && q < (int64_t)wl) img[q] = (uint8_t)(wd[t >> 2] >> (8 * (t & 3)));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- phase 2: LDS image -> destination, aligned 16-B units
+        const uint32_t nunit = (uint32_t)((wend - win + 15) / 16);
+        const uint64_t lo = (uintptr_t)dbase + r0 - ua0;  // image bytes below lo belong to another group
+        for (uint32_t u = tid; u < nunit; u += 256) {
+            const uint64_t q0 = win + 16 * (uint64_t)u;  // image offset of the unit
+            uint8_t *dst = reinterpret_cast<uint8_t *>(ua0 + q0);
+            if (q0 >= lo && q0 + 16 <= span) {
+                *reinterpret_cast<v4u *>(dst) = *reinterpret_cast<const v4u *>(img + 16 * u);
+            } else {
+                for (uint32_t t = 0; t < 16; t++)
+                    if (q0 + t >= lo && q0 + t < span) dst[t] = img[16 * u + t];
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -1453,7 +1608,22 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         timer_end("rans_encode", s);
         hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
         timer_begin("rans_compact", s);
-        hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
+        static const int cmp_old = getenv("ZR_COMPACT_OLD") ? 1 : 0;  // A/B diagnostics
+        if (cmp_old)
+            hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
+        else {
+            static const int var = getenv("ZR_CMP_VAR") ? atoi(getenv("ZR_CMP_VAR")) : 0;  // A/B diagnostics
+            if (var == 1)
+                hipLaunchKernelGGL((k_enc_compact_lds<16, 20 * 1024, 4>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
+            else if (var == 2)
+                hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 2>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
+            else if (var == 4)
+                hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 1>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
+            else if (var == 3)
+                hipLaunchKernelGGL((k_enc_compact_lds<8, 10 * 1024, 4>), dim3((uint32_t)gx * 32), dim3(256), 0, s, enc, a, w);
+            else
+                hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 4>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
+        }
         timer_end("rans_compact", s);
     }
     timer_begin("rans_encode_x1", s);
