@@ -1611,19 +1611,9 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         static const int cmp_old = getenv("ZR_COMPACT_OLD") ? 1 : 0;  // A/B diagnostics
         if (cmp_old)
             hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
-        else {
-            static const int var = getenv("ZR_CMP_VAR") ? atoi(getenv("ZR_CMP_VAR")) : 0;  // A/B diagnostics
-            if (var == 1)
-                hipLaunchKernelGGL((k_enc_compact_lds<16, 20 * 1024, 4>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
-            else if (var == 2)
-                hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 2>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
-            else if (var == 4)
-                hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 1>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
-            else if (var == 3)
-                hipLaunchKernelGGL((k_enc_compact_lds<8, 10 * 1024, 4>), dim3((uint32_t)gx * 32), dim3(256), 0, s, enc, a, w);
-            else
-                hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 4>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
-        }
+        else  // 16 streams per workgroup, 19 KiB window: 8 workgroups (32 waves) per CU
+            hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 2>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc,
+                               a, w);
         timer_end("rans_compact", s);
     }
     timer_begin("rans_encode_x1", s);
