@@ -240,16 +240,45 @@ __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tab
     d->rcp[v] = norm ? (uint32_t)(((1ull << (24 + l)) + norm - 1) / norm) : 0u;
     const uint32_t maxn = (uint32_t)__syncthreads_or(norm == TOTFREQ);
     __syncthreads();
-    for (uint32_t j = v; j < TOTFREQ; j += 256) {
-        // owner of slot j: last symbol with start <= j (zero-freq symbols share the next start)
-        int lo = 0, hi = 255;
-        while (lo < hi) {
-            int mid = (lo + hi + 1) >> 1;
-            if (start_s[mid] <= j) lo = mid;
-            else hi = mid - 1;
+    // slot owners: mark each present symbol's start, then a max-scan over the
+    // 4096 slots (thread v owns slots 16v..16v+15); zero-frequency symbols
+    // share the next start and are never marked, so the owner of slot j is
+    // the last present symbol with start <= j
+    __shared__ __attribute__((aligned(16))) uint32_t mark[TOTFREQ];
+    __shared__ uint32_t wmax[4];
+    for (uint32_t j = v; j < TOTFREQ; j += 256) mark[j] = 0;
+    __syncthreads();
+    if (norm > 0) mark[start] = v + 1;
+    __syncthreads();
+    uint32_t m[16];
+    uint32_t run = 0;
+    for (uint32_t i = 0; i < 16; i += 4) {
+        const v4u q = *reinterpret_cast<const v4u *>(&mark[16 * v + i]);
+        run = max(run, q.x); m[i] = run;
+        run = max(run, q.y); m[i + 1] = run;
+        run = max(run, q.z); m[i + 2] = run;
+        run = max(run, q.w); m[i + 3] = run;
+    }
+    uint32_t inc = run;  // inclusive max over threads <= v
+    for (uint32_t dlt = 1; dlt < 64; dlt <<= 1) {
+        const uint32_t t = __shfl_up(inc, dlt, 64);
+        if ((v & 63) >= dlt) inc = max(inc, t);
+    }
+    if ((v & 63) == 63) wmax[v >> 6] = inc;
+    __syncthreads();
+    uint32_t pre = __shfl_up(inc, 1, 64);
+    if ((v & 63) == 0) pre = 0;
+    for (uint32_t wi = 0; wi < (v >> 6); wi++) pre = max(pre, wmax[wi]);
+    v4u *dst = reinterpret_cast<v4u *>(&d->slot[16 * v]);
+    for (uint32_t i = 0; i < 16; i += 4) {
+        uint32_t o[4];
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t own = max(pre, m[i + k]) - 1;
+            const uint32_t j = 16 * v + i + k;
+            const uint32_t fs = norm_s[own];
+            o[k] = own | ((j - start_s[own]) << 8) | ((fs < TOTFREQ ? fs : 0u) << 20);
         }
-        const uint32_t fs = norm_s[lo];
-        d->slot[j] = (uint32_t)lo | ((j - start_s[lo]) << 8) | ((fs < TOTFREQ ? fs : 0u) << 20);
+        dst[i >> 2] = v4u{o[0], o[1], o[2], o[3]};
     }
     if (v == 0) {
         d->kind = maxn ? DT_SINGLE : DT_NORMAL;
@@ -683,7 +712,7 @@ __global__ __launch_bounds__(256) void k_enc_compact_lds(uint8_t *enc, KArgs a, 
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
-    if (single_mode(n, N) || a.status[b] != 0) return;
+    if (single_mode(n, N)) return;
     const uint32_t blk = grp / gpb, s0 = grp * CS;
     if (s0 >= N) return;
     const uint32_t ns = min(CS, N - s0);
@@ -692,12 +721,28 @@ __global__ __launch_bounds__(256) void k_enc_compact_lds(uint8_t *enc, KArgs a, 
     __shared__ uint32_t slen[CS], cpre[CS + 1];
     __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
     const uint32_t tid = threadIdx.x;
+    // the buffer's scan of block byte sums (k_scan, fused): this block's
+    // offset, and for group 0 the encoded length and the final status
+    uint64_t below = 0, all = 0;
+    for (uint32_t i = tid; i < nblk; i += 256) {
+        const uint64_t v = w.blocksum[(size_t)b * nblk + i];
+        below += i < blk ? v : 0;
+        all += v;
+    }
+    const uint64_t bo = block_sum(below, sh);
+    if (grp == 0) {  // workgroup-uniform
+        const uint64_t tot = block_sum(all, sh);
+        if (tid == 0) {
+            a.enc_len[b] = (uint64_t)N * 12 + tot;
+            if (a.status[b] != 0) a.status[b] = ZR_INVALID_INPUT;
+        }
+    }
+    if (a.status[b] != 0) return;  // nonzero for every reader once marked by k_enc_xn
     {
         // offsets of the block's streams (block scan), keep this group's
         const uint32_t sb = blk * 256 + tid;
         const uint32_t i = sb - s0;
         const bool mine = sb >= s0 && i < ns;
-        const uint64_t bo = w.blockoff[(size_t)b * nblk + blk];
         const uint32_t L = sb < N ? w.st_len[(size_t)b * N + sb] : 0;
         const uint32_t X = mine ? w.st_state[(size_t)b * N + sb] : 0;
         const uint64_t off = block_excl_scan(L, sh, nullptr) + bo;
@@ -1606,12 +1651,12 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         static const int ablate = getenv("ZR_ABLATE") ? atoi(getenv("ZR_ABLATE")) : 0;  // diagnostics only
         hipLaunchKernelGGL(k_enc_xn, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w, ablate);
         timer_end("rans_encode", s);
-        hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
-        timer_begin("rans_compact", s);
         static const int cmp_old = getenv("ZR_COMPACT_OLD") ? 1 : 0;  // A/B diagnostics
+        if (cmp_old) hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
+        timer_begin("rans_compact", s);
         if (cmp_old)
             hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
-        else  // 16 streams per workgroup, 19 KiB window: 8 workgroups (32 waves) per CU
+        else  // 16 streams per workgroup, 19 KiB window (8 workgroups per CU); block-sum scan fused in
             hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 2>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc,
                                a, w);
         timer_end("rans_compact", s);
