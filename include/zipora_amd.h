@@ -111,6 +111,34 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *batch, const uint8_t *raw,
 int32_t zr_rans_decode_batch_dev(const zr_rans_batch *batch, const uint8_t *enc, uint8_t *raw,
                                  void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---- RansCompressor record format (compression/mod.rs:416-512) ----
+ * record = 256 x u32 LE normalised freqs | u32 LE size | x1 stream; empty <-> empty.
+ * decompress re-normalises the stored frequencies with Rans64Encoder::new, as the
+ * reference does (mod.rs:514; not the identity for skewed tables). */
+/* RansCompressor::new(training_data): histogram + Rans64Encoder::new   mod.rs:425-452 */
+int32_t zr_rans_compressor_train(const uint8_t *train, size_t n, zr_rans_table *out);
+/* record slot size for n input bytes (header + x1 bound) */
+size_t zr_rans_compressor_bound(size_t n);
+/* Compressor::compress                                                  mod.rs:457-477 */
+int32_t zr_rans_compressor_compress(const zr_rans_table *t, const uint8_t *in, size_t n, uint8_t *out,
+                                    size_t out_cap, size_t *out_len);
+/* the stored original size of a record (0 for an empty record) */
+int32_t zr_rans_compressor_decompressed_size(const uint8_t *in, size_t n, size_t *size);
+/* Compressor::decompress                                                mod.rs:479-516 */
+int32_t zr_rans_compressor_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                                      size_t *out_len);
+/* device batches of records (blob-store put/get): x1, one compressor per batch.
+ * compress: tables = the compressor's device table, enc + enc_off[b] holds
+ * zr_rans_compressor_bound(len[b]) bytes, enc_len[b] = record length.
+ * decompress: the table is rebuilt on device from the first non-empty record's
+ * stored frequencies; len[b] must equal the stored size; a record whose stored
+ * table differs from that one gets ZR_UNSUPPORTED. */
+size_t zr_rans_compressor_workspace_bytes(uint32_t n_buffers, uint64_t max_len);
+int32_t zr_rans_compressor_compress_batch_dev(const zr_rans_batch *batch, const uint8_t *raw, uint8_t *enc,
+                                              void *workspace, size_t workspace_bytes, void *stream);
+int32_t zr_rans_compressor_decompress_batch_dev(const zr_rans_batch *batch, const uint8_t *enc, uint8_t *raw,
+                                                void *workspace, size_t workspace_bytes, void *stream);
+
 /* ---- host-resident batches (blob-store records, file buffers) ----
  * The same batch coding with every array in HOST memory: buffers are cut into
  * groups of whole buffers (<= group_bytes raw bytes, 0 = 32 MiB) that stream

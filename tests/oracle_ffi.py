@@ -137,6 +137,38 @@ def rans_decode(table, n_streams, enc, n):
     return ctypes.string_at(out, n)
 
 
+# ------------------------------------------------------- RansCompressor
+# compression/mod.rs:416-512 composed from the rANS restatement above.
+def rans_compressor_table(train):
+    """RansCompressor::new (mod.rs:425-452): byte counts (the min-1 fix-up at
+    :438-448 never fires: present symbols already count >= 1) -> Rans64Encoder::new."""
+    if not train:
+        raise OracleError("rANS compressor requires training data")
+    return rans_table(histogram(train))
+
+
+def rans_compressor_compress(table, data):
+    """Compressor::compress (mod.rs:457-477)."""
+    import struct
+    if not data:
+        return b""
+    hdr = b"".join(struct.pack("<I", table.freq[i]) for i in range(256))
+    return hdr + struct.pack("<I", len(data) & 0xFFFFFFFF) + rans_encode(table, 1, data)
+
+
+def rans_compressor_decompress(rec):
+    """Compressor::decompress (mod.rs:479-516): Rans64Encoder::new on the STORED
+    normalised frequencies (re-normalises them: finding 0.9)."""
+    import struct
+    if not rec:
+        return b""
+    if len(rec) < 1028:
+        raise OracleError("Invalid rANS compressed data format")
+    freqs = list(struct.unpack("<256I", rec[:1024]))
+    size = struct.unpack("<I", rec[1024:1028])[0]
+    return rans_decode(rans_table(freqs), 1, rec[1028:], size)
+
+
 # ---------------------------------------------------------------- FSE
 def fse_config(**kw):
     c = FseConfig()

@@ -25,3 +25,4 @@ from .fse import (EntropyStats, FseConfig, FseDecoder, FseDevice, FseEncoder,  #
                   fse_unzip, fse_zip)
 from .huffman import (ContextualHuffmanDecoder, ContextualHuffmanEncoder, HuffmanDecoder,  # noqa: F401,E402
                       HuffmanEncoder, HuffmanO1Device, HuffmanOrder, HuffmanTree, InterleavingFactor)
+from .compression import RansCompressor  # noqa: F401,E402

@@ -78,6 +78,17 @@ SIGNATURES = [
                                              c_vp]),
     ("zr_rans_pipe_decode", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                              c_vp]),
+    ("zr_rans_compressor_train", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(RansTable)]),
+    ("zr_rans_compressor_bound", c_sz, [c_sz]),
+    ("zr_rans_compressor_compress", ctypes.c_int32, [ctypes.POINTER(RansTable), c_u8p, c_sz, c_u8p, c_sz,
+                                                     ctypes.POINTER(c_sz)]),
+    ("zr_rans_compressor_decompressed_size", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_rans_compressor_decompress", ctypes.c_int32, [c_u8p, c_sz, c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_rans_compressor_workspace_bytes", c_sz, [ctypes.c_uint32, ctypes.c_uint64]),
+    ("zr_rans_compressor_compress_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp,
+                                                               c_sz, c_vp]),
+    ("zr_rans_compressor_decompress_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp,
+                                                                 c_sz, c_vp]),
     ("zr_host_register", ctypes.c_int32, [c_vp, c_sz]),
     ("zr_host_unregister", ctypes.c_int32, [c_vp]),
     ("zr_fse_config_default", None, [ctypes.POINTER(FseConfig)]),

@@ -16,7 +16,7 @@ LIB = os.path.join(PKG, "libzipora_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ZR_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["zr_api.cpp", "zr_rans.hip", "zr_fse.hip", "zr_huff.hip", "zr_pipe.cpp"]
+SOURCES = ["zr_api.cpp", "zr_rans.hip", "zr_fse.hip", "zr_huff.hip", "zr_pipe.cpp", "zr_compressor.hip"]
 HEADERS = ["zr_internal.h", os.path.join("..", "..", "include", "zipora_amd.h")]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
           "-Wno-unused-function", "-Wno-unused-variable", "-munsafe-fp-atomics"]

@@ -290,16 +290,29 @@ __device__ __forceinline__ void asm_load16(v4u &dst, uintptr_t addr) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(addr) : "memory");
 }
 
-// s_waitcnt vmcnt(min(n, 12)) with a runtime, wave-uniform n
-#define ZR_WAITC(k) \
-    case k:         \
-        asm volatile("s_waitcnt vmcnt(" #k ")" : "+v"(reg)::"memory"); \
-        break;
+// s_waitcnt vmcnt(min(n, 12)) with a runtime, wave-uniform n. One asm
+// statement with its own scalar branches: separate asm statements per count
+// let the compiler copy `reg` (still being loaded) between them.
 __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
-    switch (n > 12 ? 12 : n) {
-        ZR_WAITC(0) ZR_WAITC(1) ZR_WAITC(2) ZR_WAITC(3) ZR_WAITC(4) ZR_WAITC(5) ZR_WAITC(6)
-        ZR_WAITC(7) ZR_WAITC(8) ZR_WAITC(9) ZR_WAITC(10) ZR_WAITC(11) ZR_WAITC(12)
-    }
+    const uint32_t k = __builtin_amdgcn_readfirstlane(n > 12 ? 12u : n);
+    asm volatile(
+        "s_cmp_eq_u32 %1, 0\n\ts_cbranch_scc0 1f\n\ts_waitcnt vmcnt(0)\n\ts_branch 20f\n"
+        "1:\n\ts_cmp_eq_u32 %1, 1\n\ts_cbranch_scc0 2f\n\ts_waitcnt vmcnt(1)\n\ts_branch 20f\n"
+        "2:\n\ts_cmp_eq_u32 %1, 2\n\ts_cbranch_scc0 3f\n\ts_waitcnt vmcnt(2)\n\ts_branch 20f\n"
+        "3:\n\ts_cmp_eq_u32 %1, 3\n\ts_cbranch_scc0 4f\n\ts_waitcnt vmcnt(3)\n\ts_branch 20f\n"
+        "4:\n\ts_cmp_eq_u32 %1, 4\n\ts_cbranch_scc0 5f\n\ts_waitcnt vmcnt(4)\n\ts_branch 20f\n"
+        "5:\n\ts_cmp_eq_u32 %1, 5\n\ts_cbranch_scc0 6f\n\ts_waitcnt vmcnt(5)\n\ts_branch 20f\n"
+        "6:\n\ts_cmp_eq_u32 %1, 6\n\ts_cbranch_scc0 7f\n\ts_waitcnt vmcnt(6)\n\ts_branch 20f\n"
+        "7:\n\ts_cmp_eq_u32 %1, 7\n\ts_cbranch_scc0 8f\n\ts_waitcnt vmcnt(7)\n\ts_branch 20f\n"
+        "8:\n\ts_cmp_eq_u32 %1, 8\n\ts_cbranch_scc0 9f\n\ts_waitcnt vmcnt(8)\n\ts_branch 20f\n"
+        "9:\n\ts_cmp_eq_u32 %1, 9\n\ts_cbranch_scc0 10f\n\ts_waitcnt vmcnt(9)\n\ts_branch 20f\n"
+        "10:\n\ts_cmp_eq_u32 %1, 10\n\ts_cbranch_scc0 11f\n\ts_waitcnt vmcnt(10)\n\ts_branch 20f\n"
+        "11:\n\ts_cmp_eq_u32 %1, 11\n\ts_cbranch_scc0 12f\n\ts_waitcnt vmcnt(11)\n\ts_branch 20f\n"
+        "12:\n\ts_waitcnt vmcnt(12)\n"
+        "20:"
+        : "+v"(reg)
+        : "s"(k)
+        : "memory", "scc");
 }
 
 // ======================================================================
@@ -434,6 +447,10 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         } else {
             const uint4 v = load_piece(t);
             dst = v4u{v.x, v.y, v.z, v.w};
+            // settle the compiler's loads here: otherwise the merge with the
+            // asm-loaded path leaves dst "pending" and the tile wait below
+            // becomes vmcnt(0), which also waits for every scratch store
+            asm volatile("" : "+v"(dst));
         }
     };
     const uint64_t ntiles = (cmax + ETILE - 1) / ETILE;
@@ -441,7 +458,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     issue_piece(ntiles - 1, pend);
     for (uint64_t t = ntiles; t-- > 0;) {
         __syncthreads();
-        wait_vmcnt_le(sc, pend);
+        wait_vmcnt_le(sc, pend);  // sc is wave-uniform
         *reinterpret_cast<v4u *>(&itile[lr * 256 + lp]) = pend;
         __syncthreads();
         sc = 0;
@@ -452,8 +469,12 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
             // full tile, every lane of the wave a stream: no per-lane predicates
 #pragma unroll
             for (int g = ETILE - 4; g >= 0; g -= 4) {
-                const uint32_t s3 = itile[(g + 3) * 256 + threadIdx.x], s2 = itile[(g + 2) * 256 + threadIdx.x];
-                const uint32_t s1 = itile[(g + 1) * 256 + threadIdx.x], s0 = itile[g * 256 + threadIdx.x];
+                uint32_t s3 = itile[(g + 3) * 256 + threadIdx.x], s2 = itile[(g + 2) * 256 + threadIdx.x];
+                uint32_t s1 = itile[(g + 1) * 256 + threadIdx.x], s0 = itile[g * 256 + threadIdx.x];
+                if (ablate & 2) {  // diagnostic: conflict-free table reads (consecutive entries)
+                    const uint32_t t = (threadIdx.x + (s0 & 1)) & 255;
+                    s3 = s2 = s1 = s0 = t;
+                }
                 const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
                 enc_fast(e3);
                 enc_fast(e2);

@@ -197,3 +197,33 @@ class RansHostPipe:
                                          self._p(raw), self._p(np.ascontiguousarray(raw_off, dtype=np.uint64)),
                                          self._p(status)))
         return status
+
+
+class RansCompressorDeviceBatch(RansDeviceBatch):
+    """Device batches of RansCompressor records (compression/mod.rs:416-512): x1
+    streams behind a 1028-byte header, one compressor (shared table) per batch."""
+
+    def __init__(self, lens, device="cuda", align=16):
+        super().__init__(lens, 1, device=device, shared_table=True, align=align)
+        L = self.L
+        enc_off, e = [], 0
+        for n in self.lens_host:
+            enc_off.append(e)
+            e += (L.zr_rans_compressor_bound(n) + align - 1) // align * align
+        self.enc_bytes = e
+        self.enc_off_host = enc_off
+        self.enc_off = torch.tensor(enc_off, dtype=torch.int64, device=self.device)
+        wsb = L.zr_rans_compressor_workspace_bytes(self.B, self.max_len)
+        self.ws = torch.empty(wsb, dtype=torch.uint8, device=self.device)
+        self.ws_bytes = wsb
+        self.cbatch.enc_off = self.enc_off.data_ptr()
+
+    def compress(self, raw, enc, stream=None):
+        """Compressor::compress per record, on device (table: upload_tables / tables_from_hist)."""
+        check(self.L.zr_rans_compressor_compress_batch_dev(ctypes.byref(self.cbatch), _ptr(raw), _ptr(enc),
+                                                           _ptr(self.ws), self.ws_bytes, _stream(stream)))
+
+    def decompress(self, enc, raw, stream=None):
+        """Compressor::decompress per record, on device (table rebuilt from the stored header)."""
+        check(self.L.zr_rans_compressor_decompress_batch_dev(ctypes.byref(self.cbatch), _ptr(enc), _ptr(raw),
+                                                             _ptr(self.ws), self.ws_bytes, _stream(stream)))
