@@ -241,6 +241,23 @@ int32_t zr_huff_decode_dev(const zr_huff_tree *t, const uint8_t *in, size_t in_l
                            size_t n, int32_t *status_dev, void *workspace,
                            size_t workspace_bytes, void *stream);
 
+/* HuffmanTree::serialize / deserialize (tree.rs:226-306). serialize writes
+ * the symbols in ascending order (the reference walks a HashMap, so its bytes
+ * vary between runs; every order deserializes to the same codes). Codes over
+ * 64 bits or trees over 511 nodes (crafted input only) are ZR_UNSUPPORTED. */
+size_t zr_huff_tree_serialized_bound(void);
+int32_t zr_huff_tree_serialize(const zr_huff_tree *t, uint8_t *out, size_t out_cap, size_t *out_len);
+int32_t zr_huff_tree_deserialize(const uint8_t *in, size_t n, zr_huff_tree *t);
+/* HuffmanCompressor (compression/mod.rs:320-408): record = tree_size u32 |
+ * serialized tree | size u32 | Huffman bits; empty <-> empty */
+int32_t zr_huff_compressor_train(const uint8_t *train, size_t n, zr_huff_tree *t);
+size_t zr_huff_compressor_bound(const zr_huff_tree *t, size_t n);
+int32_t zr_huff_compressor_compress(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8_t *out,
+                                    size_t out_cap, size_t *out_len);
+int32_t zr_huff_compressor_decompressed_size(const uint8_t *in, size_t n, size_t *size);
+int32_t zr_huff_compressor_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                                      size_t *out_len);
+
 /* ======================================================================
  * Contextual Huffman order-1/2 -- src/entropy/huffman/interleaved.rs
  * Every order-1/2 context tree holds all 256 symbols (interleaved.rs:160-171),

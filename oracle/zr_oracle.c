@@ -18,6 +18,7 @@
 
 #define OK 0
 #define EINVAL_DATA (-1)
+#define EUNSUP (-4)
 
 /* ------------------------------------------------------------------------ */
 /* small growable byte vector                                                */
@@ -929,6 +930,93 @@ static size_t huff_walk(const or_huff_tree *t, const uint8_t *in, size_t in_len,
 }
 
 /* HuffmanDecoder::decode, decoder.rs:90-165 */
+/* HuffmanTree::serialize, tree.rs:226-262. The reference walks a HashMap;
+ * this restatement writes the symbols in ascending order. out holds
+ * 2 + 256 * 10 bytes. */
+size_t or_huff_tree_serialize(const or_huff_tree *t, uint8_t *out) {
+    size_t o = 2;
+    unsigned count = 0;
+    for (int s = 0; s < 256; s++) {
+        const unsigned L = t->code_len[s];
+        if (!L) continue;
+        count++;
+        out[o++] = (uint8_t)s;
+        out[o++] = (uint8_t)L;
+        uint8_t cur = 0;
+        unsigned bi = 0;
+        for (unsigned i = 0; i < L; i++) { /* pack LSB-first (tree.rs:239-256) */
+            if ((t->code[s] >> i) & 1) cur |= (uint8_t)(1u << bi);
+            if (++bi == 8) {
+                out[o++] = cur;
+                cur = 0;
+                bi = 0;
+            }
+        }
+        if (bi) out[o++] = cur;
+    }
+    out[0] = (uint8_t)count;
+    out[1] = (uint8_t)(count >> 8);
+    return o;
+}
+
+/* HuffmanTree::deserialize, tree.rs:265-306, and build_decoding_tree_from_codes,
+ * tree.rs:311-356. `order` (256 symbols, or NULL = ascending) is the HashMap
+ * iteration order the codes are inserted in. Codes over 64 bits are rejected
+ * (they do not fit the 64-bit code words of this restatement). */
+int or_huff_tree_deserialize(const uint8_t *in, size_t n, const int *order, or_huff_tree *t) {
+    memset(t, 0, sizeof(*t));
+    if (n < 2) return EINVAL_DATA; /* "Huffman tree data too short" */
+    const unsigned count = (unsigned)in[0] | ((unsigned)in[1] << 8);
+    uint8_t present[256] = {0};
+    size_t o = 2;
+    for (unsigned k = 0; k < count; k++) {
+        if (o + 2 > n) return EINVAL_DATA; /* "Truncated Huffman tree data" */
+        const uint8_t s = in[o], L = in[o + 1];
+        o += 2;
+        const size_t nb = ((size_t)L + 7) / 8;
+        if (o + nb > n) return EINVAL_DATA; /* "Truncated Huffman code data" */
+        if (L > 64) return EUNSUP;
+        uint64_t c = 0;
+        for (unsigned i = 0; i < L; i++) c |= (uint64_t)((in[o + i / 8] >> (i % 8)) & 1) << i;
+        present[s] = 1; /* HashMap::insert: a repeated symbol overwrites */
+        t->code_len[s] = L;
+        t->code[s] = c;
+        if (L > t->max_code_length) t->max_code_length = L;
+        o += nb;
+    }
+    int nsym = 0, last = 0;
+    for (int s = 0; s < 256; s++)
+        if (present[s]) {
+            nsym++;
+            last = s;
+        }
+    t->n_symbols = nsym;
+    if (nsym == 0) {
+        t->kind = 0;
+        return OK;
+    }
+    if (nsym == 1) {
+        ht_new_node(t, 1, last);
+        t->kind = 1;
+        return OK;
+    }
+    int root = ht_new_node(t, 0, 0);
+    int a = ht_new_node(t, 1, 0), b = ht_new_node(t, 1, 0);
+    memset(ph, 0, sizeof(ph));
+    ph[a] = ph[b] = 1;
+    t->node_child[root][0] = (int16_t)a;
+    t->node_child[root][1] = (int16_t)b;
+    for (int k = 0; k < 256; k++) {
+        const int s = order ? order[k] : k;
+        if (!present[s]) continue;
+        if (t->n_nodes + 2 * (int)t->code_len[s] + 2 > 1024) return EUNSUP;
+        int st = insert_code(t, root, (uint8_t)s, t->code[s], t->code_len[s], 0);
+        if (st) return st;
+    }
+    t->kind = 2;
+    return OK;
+}
+
 int or_huff_decode(const or_huff_tree *t, const uint8_t *in, size_t in_len, uint8_t *out, size_t n,
                    size_t *out_len) {
     *out_len = 0;

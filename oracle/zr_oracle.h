@@ -88,6 +88,10 @@ int or_huff_encode(const or_huff_tree *t, const uint8_t *in, size_t n, uint8_t *
 int or_huff_decode(const or_huff_tree *t, const uint8_t *in, size_t in_len, uint8_t *out,
                    size_t n, size_t *out_len);                      /* decoder.rs:90-165 */
 
+size_t or_huff_tree_serialize(const or_huff_tree *t, uint8_t *out);          /* tree.rs:226-262 */
+int or_huff_tree_deserialize(const uint8_t *in, size_t n, const int *order,
+                             or_huff_tree *t);                             /* tree.rs:265-356 */
+
 /* ---- Contextual Huffman O1/O2 (src/entropy/huffman/interleaved.rs) ---- */
 typedef struct or_ctx_huff or_ctx_huff;
 or_ctx_huff *or_ctx_new(const uint8_t *train, size_t n, int order, int *status);

@@ -71,6 +71,9 @@ def lib():
         L.or_huff_encode_bound.restype = sz
         L.or_huff_encode.argtypes = [ctypes.POINTER(HuffTree), u8p, sz, u8p, ctypes.POINTER(sz)]
         L.or_huff_decode.argtypes = [ctypes.POINTER(HuffTree), u8p, sz, u8p, sz, ctypes.POINTER(sz)]
+        L.or_huff_tree_serialize.argtypes = [ctypes.POINTER(HuffTree), u8p]
+        L.or_huff_tree_serialize.restype = sz
+        L.or_huff_tree_deserialize.argtypes = [u8p, sz, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(HuffTree)]
         L.or_ctx_new.argtypes = [u8p, sz, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.or_ctx_new.restype = ctypes.c_void_p
         L.or_ctx_free.argtypes = [ctypes.c_void_p]
@@ -239,6 +242,47 @@ def huff_decode(t, enc, n):
     ol = sz(0)
     _check(lib().or_huff_decode(ctypes.byref(t), b, ln, out, n, ctypes.byref(ol)), "huff_decode")
     return ctypes.string_at(out, ol.value)
+
+
+def huff_tree_serialize(t):
+    """HuffmanTree::serialize (tree.rs:226-262), symbols ascending."""
+    out = _out(2 + 256 * 10)
+    n = lib().or_huff_tree_serialize(ctypes.byref(t), out)
+    return ctypes.string_at(out, n)
+
+
+def huff_tree_deserialize(data, order=None):
+    """HuffmanTree::deserialize (tree.rs:265-356); `order` = HashMap insertion order."""
+    b, n = _buf(data)
+    t = HuffTree()
+    o = (ctypes.c_int * 256)(*order) if order is not None else None
+    _check(lib().or_huff_tree_deserialize(b, n, o, ctypes.byref(t)), "huff_tree_deserialize")
+    return t
+
+
+def huff_compressor_compress(t, data):
+    """HuffmanCompressor::compress (compression/mod.rs:345-369)."""
+    import struct
+    if not data:
+        return b""
+    body = huff_encode(t, data)
+    tree = huff_tree_serialize(t)
+    return struct.pack("<I", len(tree)) + tree + struct.pack("<I", len(data) & 0xFFFFFFFF) + body
+
+
+def huff_compressor_decompress(rec, order=None):
+    """HuffmanCompressor::decompress (compression/mod.rs:371-407)."""
+    import struct
+    if not rec:
+        return b""
+    if len(rec) < 8:
+        raise OracleError("Huffman compressed data too short")
+    ts = struct.unpack("<I", rec[:4])[0]
+    if len(rec) < 8 + ts:
+        raise OracleError("Huffman compressed data truncated")
+    t = huff_tree_deserialize(rec[4:4 + ts], order)
+    size = struct.unpack("<I", rec[4 + ts:8 + ts])[0]
+    return huff_decode(t, rec[8 + ts:], size)
 
 
 # ---------------------------------------------------------------- contextual

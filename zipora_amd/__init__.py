@@ -23,6 +23,6 @@ def synth(kind, n, seed=0):
 from .fse import (EntropyStats, FseConfig, FseDecoder, FseDevice, FseEncoder,  # noqa: F401,E402
                   fse_compress, fse_compress_with_config, fse_decompress, fse_decompress_with_config,
                   fse_unzip, fse_zip)
-from .huffman import (ContextualHuffmanDecoder, ContextualHuffmanEncoder, HuffmanDecoder,  # noqa: F401,E402
-                      HuffmanEncoder, HuffmanO1Device, HuffmanOrder, HuffmanTree, InterleavingFactor)
+from .huffman import (ContextualHuffmanDecoder, ContextualHuffmanEncoder, HuffmanCompressor,  # noqa: F401,E402
+                      HuffmanDecoder, HuffmanEncoder, HuffmanO1Device, HuffmanOrder, HuffmanTree, InterleavingFactor)
 from .compression import RansCompressor  # noqa: F401,E402

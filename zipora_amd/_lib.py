@@ -116,6 +116,15 @@ SIGNATURES = [
                                             c_vp, c_vp, c_sz, c_vp]),
     ("zr_huff_decode_dev", ctypes.c_int32, [ctypes.POINTER(HuffTree), c_vp, c_sz, c_vp, c_sz, c_vp,
                                             c_vp, c_sz, c_vp]),
+    ("zr_huff_tree_serialized_bound", c_sz, []),
+    ("zr_huff_tree_serialize", ctypes.c_int32, [ctypes.POINTER(HuffTree), c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_huff_tree_deserialize", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(HuffTree)]),
+    ("zr_huff_compressor_train", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(HuffTree)]),
+    ("zr_huff_compressor_bound", c_sz, [ctypes.POINTER(HuffTree), c_sz]),
+    ("zr_huff_compressor_compress", ctypes.c_int32, [ctypes.POINTER(HuffTree), c_u8p, c_sz, c_u8p, c_sz,
+                                                     ctypes.POINTER(c_sz)]),
+    ("zr_huff_compressor_decompressed_size", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_huff_compressor_decompress", ctypes.c_int32, [c_u8p, c_sz, c_u8p, c_sz, ctypes.POINTER(c_sz)]),
     ("zr_ctx_huff_new", ctypes.c_int32, [c_u8p, c_sz, ctypes.c_int32, ctypes.POINTER(c_vp)]),
     ("zr_ctx_huff_free", None, [c_vp]),
     ("zr_ctx_huff_order", ctypes.c_int32, [c_vp]),

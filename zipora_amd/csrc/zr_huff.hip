@@ -557,6 +557,72 @@ static void launch_copy(const uint8_t *src, uint8_t *dst, uint64_t n, hipStream_
     }
 }
 
+
+// build_decoding_tree_from_codes (tree.rs:311-356) + insert_code_into_tree
+// (tree.rs:359-469). Placeholder leaves (symbol 0, frequency 0) fill the
+// branches no code takes. An empty remaining code replaces the node it reaches
+// with a leaf (tree.rs:360-366), so for such inputs insertion order matters:
+// the reference iterates a HashMap, here the order is ascending symbol.
+int32_t tree_from_codes(const uint8_t present[256], const uint8_t len[256], const uint64_t code[256],
+                        zr_huff_tree *t) {
+    memset(t, 0, sizeof(*t));
+    int count = 0, last = -1;
+    uint32_t maxlen = 0;
+    for (int s = 0; s < 256; s++)
+        if (present[s]) {
+            count++;
+            last = s;
+            maxlen = std::max<uint32_t>(maxlen, len[s]);
+            t->code_len[s] = len[s];
+            t->code[s] = code[s];
+        }
+    t->n_symbols = count;
+    t->max_code_length = maxlen;
+    if (count == 0) {  // tree.rs:315-317
+        t->kind = 0;
+        return ZR_OK;
+    }
+    if (count == 1) {  // tree.rs:320-334: a single leaf whatever its code
+        t->kind = 1;
+        new_node(t, last);
+        return ZR_OK;
+    }
+    t->kind = 2;
+    std::vector<uint8_t> ph;  // placeholder flag per node
+    auto mk = [&](bool p) -> int {
+        if (t->n_nodes >= 511) return -1;
+        const int i = new_node(t, 0);
+        ph.resize(t->n_nodes);
+        ph[i] = p ? 1 : 0;
+        return i;
+    };
+    const int root = mk(false);
+    t->child[root][0] = (int16_t)mk(true);
+    t->child[root][1] = (int16_t)mk(true);
+    for (int s = 0; s < 256; s++) {
+        if (!present[s]) continue;
+        int node = root;
+        for (uint32_t i = 0;; i++) {
+            if (i == len[s]) {  // remaining code empty: this node becomes the symbol's leaf
+                t->child[node][0] = t->child[node][1] = -1;
+                t->sym[node] = (uint8_t)s;
+                ph[node] = 0;
+                break;
+            }
+            if (t->child[node][0] < 0) {  // a leaf on the path
+                if (!ph[node]) return set_error(ZR_INVALID_INPUT, "Code collision: trying to overwrite existing symbol");
+                const int a = mk(true), b = mk(true);  // placeholder -> internal node
+                if (a < 0 || b < 0) return set_error(ZR_UNSUPPORTED, "Huffman tree exceeds 511 nodes");
+                ph[node] = 0;
+                t->child[node][0] = (int16_t)a;
+                t->child[node][1] = (int16_t)b;
+            }
+            node = t->child[node][(code[s] >> i) & 1];
+        }
+    }
+    return ZR_OK;
+}
+
 }  // namespace zr
 
 using namespace zr;
@@ -913,6 +979,157 @@ int32_t zr_ctx_huff_decode(const zr_ctx_huff *h, int32_t nway, const uint8_t *in
     ZR_HIP(hipDeviceSynchronize());
     ZR_HIP(hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
     *out_len = n;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// ---- serialized trees and the HuffmanCompressor record
+
+size_t zr_huff_tree_serialized_bound(void) { return 2 + 256 * (2 + 8); }
+
+// HuffmanTree::serialize (tree.rs:226-262) with the symbols in ascending
+// order: the reference walks a HashMap, so its order (and bytes) vary from
+// run to run; any order deserializes to the same codes.
+int32_t zr_huff_tree_serialize(const zr_huff_tree *t, uint8_t *out, size_t out_cap, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!t || !out || !out_len) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    size_t need = 2;
+    uint32_t count = 0;
+    for (int s = 0; s < 256; s++)
+        if (t->code_len[s]) {
+            count++;
+            need += 2 + (t->code_len[s] + 7) / 8;
+        }
+    if (need > out_cap) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+    size_t o = 0;
+    out[o++] = (uint8_t)count;
+    out[o++] = (uint8_t)(count >> 8);
+    for (int s = 0; s < 256; s++) {
+        const uint32_t L = t->code_len[s];
+        if (!L) continue;
+        out[o++] = (uint8_t)s;
+        out[o++] = (uint8_t)L;
+        for (uint32_t k = 0; k < (L + 7) / 8; k++) {
+            const uint32_t bits = std::min<uint32_t>(8, L - 8 * k);
+            out[o++] = (uint8_t)((t->code[s] >> (8 * k)) & ((1u << bits) - 1));
+        }
+    }
+    *out_len = o;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+// HuffmanTree::deserialize (tree.rs:265-306). Codes longer than 64 bits
+// (never produced by serialize: longer chains take the fixed 8-bit tree) are
+// ZR_UNSUPPORTED, as are crafted code sets needing more than 511 tree nodes.
+int32_t zr_huff_tree_deserialize(const uint8_t *in, size_t n, zr_huff_tree *t) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!t || (!in && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    if (n < 2) return set_error(ZR_INVALID_INPUT, "Huffman tree data too short");
+    const uint32_t count = (uint32_t)in[0] | ((uint32_t)in[1] << 8);
+    uint8_t present[256] = {}, len[256] = {};
+    uint64_t code[256] = {};
+    size_t o = 2;
+    for (uint32_t k = 0; k < count; k++) {
+        if (o + 2 > n) return set_error(ZR_INVALID_INPUT, "Truncated Huffman tree data");
+        const uint8_t s = in[o], L = in[o + 1];
+        o += 2;
+        const size_t nb = (L + 7) / 8;
+        if (o + nb > n) return set_error(ZR_INVALID_INPUT, "Truncated Huffman code data");
+        if (L > 64) return set_error(ZR_UNSUPPORTED, "Huffman code longer than 64 bits");
+        uint64_t c = 0;
+        for (size_t i = 0; i < L; i++) c |= (uint64_t)((in[o + i / 8] >> (i % 8)) & 1) << i;
+        present[s] = 1;  // a repeated symbol overwrites (HashMap::insert)
+        len[s] = L;
+        code[s] = c;
+        o += nb;
+    }
+    return tree_from_codes(present, len, code, t);
+    ZR_GUARD_END
+}
+
+// HuffmanCompressor::new (compression/mod.rs:330-334): HuffmanEncoder::new(training_data)
+int32_t zr_huff_compressor_train(const uint8_t *train, size_t n, zr_huff_tree *t) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!t || (!train && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    uint32_t f[256];
+    int32_t st = zr_byte_histogram(train, n, f);
+    if (st) return st;
+    return huff_build(f, t);
+    ZR_GUARD_END
+}
+
+size_t zr_huff_compressor_bound(const zr_huff_tree *t, size_t n) {
+    return 8 + zr_huff_tree_serialized_bound() + zr_huff_encode_bound(t, n);
+}
+
+// Compressor::compress (mod.rs:345-369): tree_size u32 | tree | size u32 | bits
+int32_t zr_huff_compressor_compress(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8_t *out,
+                                    size_t out_cap, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!t || (!in && n) || !out_len || (!out && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    if (n == 0) return ZR_OK;
+    uint8_t tree[2 + 256 * 10];
+    size_t ts = 0;
+    int32_t st = zr_huff_tree_serialize(t, tree, sizeof(tree), &ts);
+    if (st) return st;
+    if (out_cap < 8 + ts) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+    size_t body = 0;
+    if ((st = zr_huff_encode(t, in, n, out + 8 + ts, out_cap - 8 - ts, &body))) return st;
+    for (int k = 0; k < 4; k++) out[k] = (uint8_t)(ts >> (8 * k));
+    memcpy(out + 4, tree, ts);
+    for (int k = 0; k < 4; k++) out[4 + ts + k] = (uint8_t)((uint32_t)n >> (8 * k));
+    *out_len = 8 + ts + body;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+static int32_t huff_record_parse(const uint8_t *in, size_t n, size_t *ts, size_t *size) {
+    if (n < 8) return set_error(ZR_INVALID_INPUT, "Huffman compressed data too short");  // mod.rs:376-380
+    *ts = (size_t)in[0] | ((size_t)in[1] << 8) | ((size_t)in[2] << 16) | ((size_t)in[3] << 24);
+    if (n < 8 + *ts) return set_error(ZR_INVALID_INPUT, "Huffman compressed data truncated");  // :385-389
+    const uint8_t *p = in + 4 + *ts;
+    *size = (size_t)p[0] | ((size_t)p[1] << 8) | ((size_t)p[2] << 16) | ((size_t)p[3] << 24);
+    return ZR_OK;
+}
+
+int32_t zr_huff_compressor_decompressed_size(const uint8_t *in, size_t n, size_t *size) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!size || (!in && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *size = 0;
+    if (n == 0) return ZR_OK;
+    size_t ts = 0;
+    return huff_record_parse(in, n, &ts, size);
+    ZR_GUARD_END
+}
+
+// Compressor::decompress (mod.rs:371-407): the record's own tree decodes it
+int32_t zr_huff_compressor_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                                      size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!out_len || (!in && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    if (n == 0) return ZR_OK;
+    size_t ts = 0, size = 0;
+    int32_t st = huff_record_parse(in, n, &ts, &size);
+    if (st) return st;
+    zr_huff_tree t;
+    if ((st = zr_huff_tree_deserialize(in + 4, ts, &t))) return st;
+    if (size > out_cap || (!out && size)) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+    if ((st = zr_huff_decode(&t, in + 8 + ts, n - 8 - ts, out, size))) return st;
+    *out_len = size;
     return ZR_OK;
     ZR_GUARD_END
 }

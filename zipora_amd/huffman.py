@@ -60,6 +60,24 @@ class HuffmanTree:
     def raw(self):
         return self._t
 
+    def serialize(self):
+        """HuffmanTree::serialize (tree.rs:226-262), symbols in ascending order."""
+        L = _lib.load()
+        cap = L.zr_huff_tree_serialized_bound()
+        out = (ctypes.c_uint8 * cap)()
+        ol = ctypes.c_size_t(0)
+        check(L.zr_huff_tree_serialize(ctypes.byref(self._t), out, cap, ctypes.byref(ol)))
+        return ctypes.string_at(out, ol.value)
+
+    @classmethod
+    def deserialize(cls, data):
+        """HuffmanTree::deserialize (tree.rs:265-306)."""
+        data = bytes(data)
+        buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+        t = _lib.HuffTree()
+        check(_lib.load().zr_huff_tree_deserialize(buf, len(data), ctypes.byref(t)))
+        return cls(t)
+
 
 class HuffmanEncoder:
     def __init__(self, data=None, tree=None):
@@ -238,3 +256,43 @@ class HuffmanO1Device:
 
 __all__ = ["HuffmanTree", "HuffmanEncoder", "HuffmanDecoder", "HuffmanOrder", "InterleavingFactor",
            "ContextualHuffmanEncoder", "ContextualHuffmanDecoder", "HuffmanO1Device", "ZiporaError"]
+
+
+class HuffmanCompressor:
+    """HuffmanCompressor (compression/mod.rs:320-408): tree_size u32 | serialized
+    tree | size u32 | bits; decompress uses the record's own tree."""
+
+    def __init__(self, training_data):
+        data = bytes(training_data)
+        buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+        t = _lib.HuffTree()
+        check(_lib.load().zr_huff_compressor_train(buf, len(data), ctypes.byref(t)))
+        self.tree = HuffmanTree(t)
+
+    def tree_data(self):
+        return self.tree.serialize()
+
+    def compress(self, data):
+        L = _lib.load()
+        data = bytes(data)
+        buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+        cap = L.zr_huff_compressor_bound(ctypes.byref(self.tree.raw), len(data))
+        out = (ctypes.c_uint8 * cap)()
+        ol = ctypes.c_size_t(0)
+        check(L.zr_huff_compressor_compress(ctypes.byref(self.tree.raw), buf, len(data), out, cap,
+                                            ctypes.byref(ol)))
+        return ctypes.string_at(out, ol.value)
+
+    def decompress(self, data):
+        L = _lib.load()
+        data = bytes(data)
+        buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+        size = ctypes.c_size_t(0)
+        check(L.zr_huff_compressor_decompressed_size(buf, len(data), ctypes.byref(size)))
+        out = (ctypes.c_uint8 * max(1, size.value))()
+        ol = ctypes.c_size_t(0)
+        check(L.zr_huff_compressor_decompress(buf, len(data), out, size.value, ctypes.byref(ol)))
+        return ctypes.string_at(out, ol.value)
+
+    def algorithm(self):
+        return "Huffman"  # Algorithm::Huffman (mod.rs:404-406)
