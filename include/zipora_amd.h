@@ -270,6 +270,12 @@ int32_t zr_huff_compressor_decompress(const uint8_t *in, size_t n, uint8_t *out,
 typedef struct zr_ctx_huff zr_ctx_huff;
 /* ContextualHuffmanEncoder::new(data, order)             interleaved.rs:94-266 */
 int32_t zr_ctx_huff_new(const uint8_t *train, size_t n, int32_t order, zr_ctx_huff **out);
+/* ContextualHuffmanEncoder::serialize / deserialize (interleaved.rs:476-595):
+ * contexts ascending, context k owns tree k + 1 (the reference numbers and
+ * lists them in HashMap order). */
+size_t zr_ctx_huff_serialized_size(const zr_ctx_huff *h);
+int32_t zr_ctx_huff_serialize(const zr_ctx_huff *h, uint8_t *out, size_t out_cap, size_t *out_len);
+int32_t zr_ctx_huff_deserialize(const uint8_t *in, size_t n, zr_ctx_huff **out);
 void zr_ctx_huff_free(zr_ctx_huff *h);
 int32_t zr_ctx_huff_order(const zr_ctx_huff *h);        /* effective order */
 size_t zr_ctx_huff_encode_bound(const zr_ctx_huff *h, size_t n);

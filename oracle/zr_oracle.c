@@ -1109,12 +1109,15 @@ static or_ctx_huff *ctx_new_o2(const uint8_t *d, size_t n, int *st) {
     int nctx = 0;
     for (int c = 0; c < 65536; c++)
         if (tot[c]) order[nctx++] = c;
-    /* selection sort by descending total (only top 1024 needed) */
+    /* selection sort by descending total, ties by ascending context (the
+     * reference's ties follow HashMap order); only the top 1024 are needed */
     int take = nctx < 1024 ? nctx : 1024;
     for (int i = 0; i < take; i++) {
         int best = i;
         for (int j = i + 1; j < nctx; j++)
-            if (tot[order[j]] > tot[order[best]]) best = j;
+            if (tot[order[j]] > tot[order[best]] ||
+                (tot[order[j]] == tot[order[best]] && order[j] < order[best]))
+                best = j;
         int32_t tmp = order[i];
         order[i] = order[best];
         order[best] = tmp;
@@ -1155,6 +1158,43 @@ void or_ctx_free(or_ctx_huff *c) {
     free(c);
 }
 int or_ctx_order(const or_ctx_huff *c) { return c->order; }
+
+/* ContextualHuffmanEncoder::serialize, interleaved.rs:476-503. The reference
+ * walks its context HashMap and numbers trees in HashMap order; here contexts
+ * ascend, context k is listed with tree index k + 1, and the trees follow as
+ * trees[0] then the contexts' trees in that order. */
+static int ctx_tree_of(const or_ctx_huff *c, int ctx) {
+    return c->order == 1 ? c->map1[ctx] : c->map2[ctx];
+}
+size_t or_ctx_serialize(const or_ctx_huff *c, uint8_t *out) {
+    const int nctx_all = c->order == 0 ? 0 : (c->order == 1 ? 256 : 65536);
+    uint32_t nctx = 0;
+    for (int x = 0; x < nctx_all; x++)
+        if (ctx_tree_of(c, x) >= 0) nctx++;
+    size_t o = 0;
+    out[o++] = (uint8_t)c->order;
+    const uint32_t ntrees = 1 + nctx;
+    for (int k = 0; k < 4; k++) out[o++] = (uint8_t)(ntrees >> (8 * k));
+    for (int k = 0; k < 4; k++) out[o++] = (uint8_t)(nctx >> (8 * k));
+    uint32_t idx = 1;
+    for (int x = 0; x < nctx_all; x++) {
+        if (ctx_tree_of(c, x) < 0) continue;
+        for (int k = 0; k < 4; k++) out[o++] = (uint8_t)((uint32_t)x >> (8 * k));
+        for (int k = 0; k < 4; k++) out[o++] = (uint8_t)(idx >> (8 * k));
+        idx++;
+    }
+    uint8_t *buf = (uint8_t *)malloc(2 + 256 * 10);
+    for (int x = -1; x < nctx_all; x++) {
+        const int ti = x < 0 ? 0 : ctx_tree_of(c, x);
+        if (ti < 0) continue;
+        const size_t ts = or_huff_tree_serialize(&c->trees[ti], buf);
+        for (int k = 0; k < 4; k++) out[o++] = (uint8_t)((uint32_t)ts >> (8 * k));
+        memcpy(out + o, buf, ts);
+        o += ts;
+    }
+    free(buf);
+    return o;
+}
 
 static const or_huff_tree *ctx_tree(const or_ctx_huff *c, uint32_t context) {
     int32_t ti = -1;

@@ -97,6 +97,9 @@ typedef struct or_ctx_huff or_ctx_huff;
 or_ctx_huff *or_ctx_new(const uint8_t *train, size_t n, int order, int *status);
 void or_ctx_free(or_ctx_huff *c);
 int or_ctx_order(const or_ctx_huff *c);
+/* ContextualHuffmanEncoder::serialize (interleaved.rs:476-503), canonical order;
+ * out holds 9 + 8 * 65536 + 65537 * (4 + 2562) bytes at most */
+size_t or_ctx_serialize(const or_ctx_huff *c, uint8_t *out);
 size_t or_ctx_encode_bound(const or_ctx_huff *c, const uint8_t *in, size_t n);
 int or_ctx_encode(const or_ctx_huff *c, const uint8_t *in, size_t n, uint8_t *out, size_t *out_len);
 int or_ctx_encode_xn(const or_ctx_huff *c, int nway, const uint8_t *in, size_t n, uint8_t *out,

@@ -77,6 +77,8 @@ def lib():
         L.or_ctx_new.argtypes = [u8p, sz, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.or_ctx_new.restype = ctypes.c_void_p
         L.or_ctx_free.argtypes = [ctypes.c_void_p]
+        L.or_ctx_serialize.argtypes = [ctypes.c_void_p, u8p]
+        L.or_ctx_serialize.restype = sz
         L.or_ctx_order.argtypes = [ctypes.c_void_p]
         L.or_ctx_encode_bound.argtypes = [ctypes.c_void_p, u8p, sz]
         L.or_ctx_encode_bound.restype = sz
@@ -321,6 +323,12 @@ class Ctx:
         ol = sz(0)
         _check(lib().or_ctx_decode(self.h, b, ln, out, n, ctypes.byref(ol)), "ctx_decode")
         return ctypes.string_at(out, ol.value)
+
+    def serialize(self):
+        """ContextualHuffmanEncoder::serialize (interleaved.rs:476-503), canonical order."""
+        out = _out(9 + 8 * 1024 + 1025 * (4 + 2 + 256 * 10))  # order 2 keeps <= 1024 contexts
+        n = lib().or_ctx_serialize(self.h, out)
+        return ctypes.string_at(out, n)
 
     def decode_xn(self, nway, enc, n):
         b, ln = _buf(enc)

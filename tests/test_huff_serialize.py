@@ -124,3 +124,42 @@ def test_huffman_compressor_records(zr, oracle):
             oracle.huff_compressor_decompress(bad)
     with pytest.raises(zr.ZiporaError):
         c.compress(b"abd")  # 'd' is not in the tree
+
+
+def _ctx_cases(zr):
+    text = zr.synth("t", 30000, seed=8)
+    return [(text, 0), (text, 1), (text, 2), (b"ab", 2), (b"a", 1), (b"", 0), (bytes(range(256)) * 3, 2),
+            (zr.synth("u", 300000, seed=9), 2)]  # > 1024 order-2 contexts: the top-1024 cut
+
+
+def test_oracle_ctx_serialize_layout(zr, oracle):
+    c = oracle.Ctx(b"abcab", 1)
+    ser = c.serialize()
+    order, ntrees, nctx = ser[0], *struct.unpack("<II", ser[1:9])
+    assert (order, ntrees, nctx) == (1, 4, 3)  # contexts a, b, c precede a symbol
+    pairs = [struct.unpack("<II", ser[9 + 8 * k:17 + 8 * k]) for k in range(nctx)]
+    assert pairs == [(0x61, 1), (0x62, 2), (0x63, 3)]
+
+
+@pytest.mark.gpu
+def test_ctx_serialize_parity(zr, oracle):
+    for train, order in _ctx_cases(zr):
+        enc = zr.ContextualHuffmanEncoder(train, order)
+        ser = enc.serialize()
+        assert ser == oracle.Ctx(train, order).serialize(), (len(train), order)
+        back = zr.ContextualHuffmanEncoder.deserialize(ser)
+        assert back.order() == enc.order()
+        assert back.serialize() == ser
+        data = train[:5000]
+        if data:  # (drawn from the training bytes: every symbol has a code)
+            e = enc.encode(data)
+            assert back.encode(data) == e
+            assert zr.ContextualHuffmanDecoder(back).decode(e, len(data)) == data
+
+
+@pytest.mark.gpu
+def test_ctx_deserialize_errors(zr):
+    good = zr.ContextualHuffmanEncoder(b"hello world", 1).serialize()
+    for bad in (b"", b"\x03" + good[1:], good[:3], good[:8], good[:12], good[:-1]):
+        with pytest.raises(zr.ZiporaError):
+            zr.ContextualHuffmanEncoder.deserialize(bad)

@@ -127,6 +127,9 @@ SIGNATURES = [
     ("zr_huff_compressor_decompress", ctypes.c_int32, [c_u8p, c_sz, c_u8p, c_sz, ctypes.POINTER(c_sz)]),
     ("zr_ctx_huff_new", ctypes.c_int32, [c_u8p, c_sz, ctypes.c_int32, ctypes.POINTER(c_vp)]),
     ("zr_ctx_huff_free", None, [c_vp]),
+    ("zr_ctx_huff_serialized_size", c_sz, [c_vp]),
+    ("zr_ctx_huff_serialize", ctypes.c_int32, [c_vp, c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_ctx_huff_deserialize", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(c_vp)]),
     ("zr_ctx_huff_order", ctypes.c_int32, [c_vp]),
     ("zr_ctx_huff_encode_bound", c_sz, [c_vp, c_sz]),
     ("zr_ctx_huff_encode", ctypes.c_int32, [c_vp, ctypes.c_int32, c_u8p, c_sz, c_u8p, c_sz,

@@ -628,8 +628,9 @@ int32_t tree_from_codes(const uint8_t present[256], const uint8_t len[256], cons
 using namespace zr;
 
 struct zr_ctx_huff {
-    int32_t order;     // effective order
-    zr_huff_tree t0;   // order 0: the model; order 1/2: trees[0] (all 256 symbols)
+    int32_t order;              // effective order
+    zr_huff_tree t0;            // order 0: the model; order 1/2: trees[0] (all 256 symbols)
+    std::vector<uint32_t> ctx;  // order 1/2: the contexts that own a tree, ascending
 };
 
 extern "C" {
@@ -864,6 +865,26 @@ int32_t zr_ctx_huff_new(const uint8_t *train, size_t n, int32_t order, zr_ctx_hu
     if (st) {
         delete h;
         return st;
+    }
+    if (eff == 1) {  // one tree per context seen before a symbol (interleaved.rs:140-185)
+        uint8_t seen[256] = {};
+        for (size_t i = 1; i < n; i++) seen[train[i - 1]] = 1;
+        for (uint32_t c = 0; c < 256; c++)
+            if (seen[c]) h->ctx.push_back(c);
+    } else if (eff == 2) {
+        // the 1024 contexts with the most symbols (interleaved.rs:213-232); the
+        // reference breaks ties in HashMap order, here by ascending context
+        std::vector<uint32_t> tot(65536, 0);
+        for (size_t i = 2; i < n; i++) tot[((uint32_t)train[i - 2] << 8) | train[i - 1]]++;
+        std::vector<uint32_t> all;
+        for (uint32_t c = 0; c < 65536; c++)
+            if (tot[c]) all.push_back(c);
+        const size_t take = std::min<size_t>(1024, all.size());
+        std::partial_sort(all.begin(), all.begin() + take, all.end(), [&](uint32_t x, uint32_t y) {
+            return tot[x] != tot[y] ? tot[x] > tot[y] : x < y;
+        });
+        h->ctx.assign(all.begin(), all.begin() + take);
+        std::sort(h->ctx.begin(), h->ctx.end());
     }
     *out = h;
     return ZR_OK;
@@ -1130,6 +1151,117 @@ int32_t zr_huff_compressor_decompress(const uint8_t *in, size_t n, uint8_t *out,
     if (size > out_cap || (!out && size)) return set_error(ZR_INVALID_INPUT, "output buffer too small");
     if ((st = zr_huff_decode(&t, in + 8 + ts, n - 8 - ts, out, size))) return st;
     *out_len = size;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// ContextualHuffmanEncoder::serialize (interleaved.rs:476-503): order u8 |
+// tree count u32 | context count u32 | (context u32, tree index u32)* |
+// (tree size u32, HuffmanTree::serialize)*. The reference walks its context
+// HashMap (and numbers trees in HashMap order); here contexts ascend and
+// context k owns tree k + 1.
+size_t zr_ctx_huff_serialized_size(const zr_ctx_huff *h) {
+    uint8_t tmp[2 + 256 * 10];
+    size_t ts = 0;
+    if (!h || zr_huff_tree_serialize(&h->t0, tmp, sizeof(tmp), &ts)) return 0;
+    return 9 + 8 * h->ctx.size() + (1 + h->ctx.size()) * (4 + ts);
+}
+
+int32_t zr_ctx_huff_serialize(const zr_ctx_huff *h, uint8_t *out, size_t out_cap, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!h || !out || !out_len) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    uint8_t tree[2 + 256 * 10];
+    size_t ts = 0;
+    int32_t st = zr_huff_tree_serialize(&h->t0, tree, sizeof(tree), &ts);
+    if (st) return st;
+    const size_t need = 9 + 8 * h->ctx.size() + (1 + h->ctx.size()) * (4 + ts);
+    if (need > out_cap) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+    size_t o = 0;
+    auto put32 = [&](uint32_t v) {
+        for (int k = 0; k < 4; k++) out[o++] = (uint8_t)(v >> (8 * k));
+    };
+    out[o++] = (uint8_t)h->order;
+    put32((uint32_t)(1 + h->ctx.size()));
+    put32((uint32_t)h->ctx.size());
+    for (size_t k = 0; k < h->ctx.size(); k++) {
+        put32(h->ctx[k]);
+        put32((uint32_t)(k + 1));
+    }
+    // trees[0] and every context tree: all the same fixed 8-bit identity code for
+    // order 1/2 (every merged table has all 256 symbols); order 0 has only trees[0]
+    for (size_t k = 0; k < 1 + h->ctx.size(); k++) {
+        put32((uint32_t)ts);
+        memcpy(out + o, tree, ts);
+        o += ts;
+    }
+    *out_len = o;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+// ContextualHuffmanEncoder::deserialize (interleaved.rs:506-595). Order 1/2
+// models must consist of fixed 8-bit identity trees, which is what every
+// serialized order-1/2 model holds; anything else is ZR_UNSUPPORTED, as is a
+// model without trees.
+int32_t zr_ctx_huff_deserialize(const uint8_t *in, size_t n, zr_ctx_huff **out) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!out || (!in && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out = nullptr;
+    if (n == 0) return set_error(ZR_INVALID_INPUT, "Empty contextual Huffman data");
+    const uint8_t order = in[0];
+    if (order > 2) return set_error(ZR_INVALID_INPUT, "Invalid Huffman order");
+    size_t o = 1;
+    auto get32 = [&](uint32_t *v) {
+        *v = (uint32_t)in[o] | ((uint32_t)in[o + 1] << 8) | ((uint32_t)in[o + 2] << 16) | ((uint32_t)in[o + 3] << 24);
+        o += 4;
+    };
+    uint32_t ntrees, nctx;
+    if (o + 4 > n) return set_error(ZR_INVALID_INPUT, "Truncated tree count");
+    get32(&ntrees);
+    if (o + 4 > n) return set_error(ZR_INVALID_INPUT, "Truncated context count");
+    get32(&nctx);
+    std::vector<uint32_t> ctx;
+    for (uint32_t k = 0; k < nctx; k++) {
+        if (o + 8 > n) return set_error(ZR_INVALID_INPUT, "Truncated context map");
+        uint32_t c, idx;
+        get32(&c);
+        get32(&idx);
+        ctx.push_back(c);
+    }
+    std::sort(ctx.begin(), ctx.end());
+    ctx.erase(std::unique(ctx.begin(), ctx.end()), ctx.end());  // HashMap keys
+    zr_ctx_huff *h = new zr_ctx_huff();
+    h->order = order;
+    h->ctx = ctx;
+    auto fail = [&](int32_t st) {
+        delete h;
+        return st;
+    };
+    for (uint32_t k = 0; k < ntrees; k++) {
+        uint32_t ts;
+        if (o + 4 > n) return fail(set_error(ZR_INVALID_INPUT, "Truncated tree size"));
+        get32(&ts);
+        if (o + ts > n) return fail(set_error(ZR_INVALID_INPUT, "Truncated tree data"));
+        zr_huff_tree t;
+        int32_t st = zr_huff_tree_deserialize(in + o, ts, &t);
+        if (st) return fail(st);
+        o += ts;
+        if (order != 0) {
+            bool ident = t.kind == 2;
+            for (int s = 0; s < 256 && ident; s++) ident = t.code_len[s] == 8 && t.code[s] == (uint64_t)s;
+            if (!ident) return fail(set_error(ZR_UNSUPPORTED, "order-1/2 model with a non-identity tree"));
+        }
+        if (k == 0) h->t0 = t;
+    }
+    if (ntrees == 0) return fail(set_error(ZR_UNSUPPORTED, "contextual Huffman model without trees"));
+    *out = h;
     return ZR_OK;
     ZR_GUARD_END
 }

@@ -12,6 +12,7 @@ The tree is built by host C++ in libzipora_amd.so (<= 256 leaves); every
 encode/decode runs in HIP kernels (zr_huff.hip). Errors raise ZiporaError.
 """
 import ctypes
+import struct
 import enum
 
 from . import _lib
@@ -169,7 +170,28 @@ class ContextualHuffmanEncoder:
         return HuffmanOrder(_lib.load().zr_ctx_huff_order(self._h))
 
     def tree_count(self):
-        return 1 if self.order() == HuffmanOrder.Order0 else None  # context trees are implicit
+        """trees.len(): trees[0] plus one tree per context (interleaved.rs:94-266)."""
+        return struct.unpack("<I", self.serialize()[1:5])[0]
+
+    def serialize(self):
+        """ContextualHuffmanEncoder::serialize (interleaved.rs:476-503), contexts ascending."""
+        L = _lib.load()
+        cap = L.zr_ctx_huff_serialized_size(self._h)
+        out = (ctypes.c_uint8 * max(1, cap))()
+        ol = ctypes.c_size_t(0)
+        check(L.zr_ctx_huff_serialize(self._h, out, cap, ctypes.byref(ol)))
+        return ctypes.string_at(out, ol.value)
+
+    @classmethod
+    def deserialize(cls, data):
+        """ContextualHuffmanEncoder::deserialize (interleaved.rs:506-595)."""
+        L = _lib.load()
+        buf, n = _u8(data)
+        h = ctypes.c_void_p()
+        check(L.zr_ctx_huff_deserialize(buf, n, ctypes.byref(h)))
+        self = cls.__new__(cls)
+        self._h = h
+        return self
 
     def _encode(self, nway, data):
         L = _lib.load()
