@@ -188,6 +188,17 @@ int32_t zr_fse_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_
  * dictionary counts (fse.rs:807-812). freqs == NULL: histogram of in. */
 int32_t zr_fse_compress_freqs(const zr_fse_config *c, const uint32_t *freqs, const uint8_t *in,
                               size_t n, uint8_t *out, size_t out_cap, size_t *out_len);
+/* FSE as the PA-Zip second stage (dict_zip/compression_types.rs:2272-2340):
+ * apply = "UN" | raw below 32 bytes or when FSE does not shrink, else
+ * "FS" | FseCompressor::compress; remove inverts it ("UN", "FS", or no magic =
+ * the whole input is an FSE stream; < 2 bytes pass through). The config is
+ * dict_zip's (parallel_blocks None, 64 KiB blocks/tables, :2107-2123). */
+size_t zr_pazip_fse_bound(size_t n, const zr_fse_config *c);
+int32_t zr_pazip_fse_apply(const zr_fse_config *c, const uint8_t *in, size_t n, uint8_t *out,
+                           size_t out_cap, size_t *out_len);
+int32_t zr_pazip_fse_removed_size(const uint8_t *in, size_t n, size_t *size);
+int32_t zr_pazip_fse_remove(const zr_fse_config *c, const uint8_t *in, size_t n, uint8_t *out,
+                            size_t out_cap, size_t *out_len);
 /* analyze_frequencies' byte histogram (fse.rs:796-851) on the device */
 int32_t zr_byte_histogram(const uint8_t *in, size_t n, uint32_t freqs[256]);
 /* decoded length of a stream (parses the framing on the host) */
@@ -270,6 +281,17 @@ int32_t zr_huff_compressor_decompress(const uint8_t *in, size_t n, uint8_t *out,
 typedef struct zr_ctx_huff zr_ctx_huff;
 /* ContextualHuffmanEncoder::new(data, order)             interleaved.rs:94-266 */
 int32_t zr_ctx_huff_new(const uint8_t *train, size_t n, int32_t order, zr_ctx_huff **out);
+/* DictZipBlobStore entropy stage (dict_zip/blob_store.rs:1075-1224): algo 0
+ * None, 1 HuffmanO1 (o1_model = ContextualHuffmanEncoder over the dictionary,
+ * order 1), 2 Fse (parallel_blocks = interleave when > 1). encode keeps the
+ * entropy form only when its size / n (f32) <= ratio_require and reports the
+ * algorithm used; decode uses the non-interleaved O1 decoder with the record's
+ * original size, as the reference does (:1179-1206). */
+int32_t zr_dictzip_entropy_encode(int32_t algo, int32_t interleave, const zr_ctx_huff *o1_model,
+                                  float ratio_require, const uint8_t *in, size_t n, uint8_t *out,
+                                  size_t out_cap, size_t *out_len, int32_t *algo_used);
+int32_t zr_dictzip_entropy_decode(int32_t algo, const zr_ctx_huff *o1_model, const uint8_t *in, size_t n,
+                                  size_t original_size, uint8_t *out, size_t out_cap, size_t *out_len);
 /* ContextualHuffmanEncoder::serialize / deserialize (interleaved.rs:476-595):
  * contexts ascending, context k owns tree k + 1 (the reference numbers and
  * lists them in HashMap order). */

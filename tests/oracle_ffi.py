@@ -287,6 +287,65 @@ def huff_compressor_decompress(rec, order=None):
     return huff_decode(t, rec[8 + ts:], size)
 
 
+# ------------------------------------------------- PA-Zip / DictZip stages
+def pazip_fse_config(table_log=12, compression_level=3, adaptive=True):
+    """dict_zip FseConfig::to_entropy_config (compression_types.rs:2107-2123)."""
+    return fse_config(table_log=table_log, compression_level=compression_level, adaptive=int(adaptive),
+                      parallel_blocks=0, block_size=64 * 1024, max_table_size=64 * 1024)
+
+
+def pazip_apply(data, cfg):
+    """apply_fse_compression (compression_types.rs:2272-2299)."""
+    if not data:
+        return b""
+    if len(data) < 32:
+        return b"UN" + data
+    if not (5 <= cfg.table_log <= 15 and 1 <= cfg.compression_level <= 22):
+        raise OracleError("invalid FSE config")
+    comp = fse_compress(data, cfg)
+    return b"\xfeS" + comp if len(comp) < len(data) else b"UN" + data
+
+
+def pazip_remove(data, cfg):
+    """remove_fse_compression (compression_types.rs:2310-2340)."""
+    if not data:
+        return b""
+    if len(data) < 2:
+        return data
+    if data[:2] == b"UN":
+        return data[2:]
+    if not (5 <= cfg.table_log <= 15 and 1 <= cfg.compression_level <= 22):
+        raise OracleError("invalid FSE config")
+    body = data[2:] if data[:2] == b"\xfeS" else data
+    return fse_decompress(body) if body else b""
+
+
+def dictzip_encode(algo, interleave, ctx, ratio, data):
+    """apply_entropy_encoding + check_compression_ratio (blob_store.rs:1075-1161, :1292-1304)."""
+    import numpy as np
+    if algo == 0:
+        return data, 0
+    if algo == 1:
+        nway = {0: 1, 1: 1, 2: 2, 4: 4, 8: 8}.get(interleave)
+        if nway is None:
+            raise OracleError("Invalid interleaving factor")
+        enc = ctx.encode(data) if nway == 1 else ctx.encode_xn(nway, data)
+    else:
+        enc = fse_compress(data, fse_config(parallel_blocks=interleave if interleave > 1 else 0))
+    if data and np.float32(len(enc)) / np.float32(len(data)) <= np.float32(ratio):
+        return enc, algo
+    return data, 0
+
+
+def dictzip_decode(algo, ctx, data, original_size):
+    """decode_entropy (blob_store.rs:1164-1224): O1 with the plain decoder and original_size."""
+    if algo == 0:
+        return data
+    if algo == 1:
+        return ctx.decode(data, original_size)
+    return fse_decompress(data)
+
+
 # ---------------------------------------------------------------- contextual
 class Ctx:
     def __init__(self, train, order):

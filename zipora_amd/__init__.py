@@ -26,3 +26,5 @@ from .fse import (EntropyStats, FseConfig, FseDecoder, FseDevice, FseEncoder,  #
 from .huffman import (ContextualHuffmanDecoder, ContextualHuffmanEncoder, HuffmanCompressor,  # noqa: F401,E402
                       HuffmanDecoder, HuffmanEncoder, HuffmanO1Device, HuffmanOrder, HuffmanTree, InterleavingFactor)
 from .compression import RansCompressor  # noqa: F401,E402
+from .pazip import (DictZipEntropyStage, EntropyAlgorithm, PaZipFseConfig,  # noqa: F401,E402
+                    apply_fse_compression, remove_fse_compression)

@@ -106,6 +106,16 @@ SIGNATURES = [
     ("zr_fse_decode_workspace_bytes", c_sz, [ctypes.c_uint64]),
     ("zr_fse_decompress_dev", ctypes.c_int32, [c_vp, c_sz, c_vp, c_sz, ctypes.c_uint64, c_vp, c_vp,
                                                c_vp, c_sz, c_vp]),
+    ("zr_pazip_fse_bound", c_sz, [c_sz, ctypes.POINTER(FseConfig)]),
+    ("zr_pazip_fse_apply", ctypes.c_int32, [ctypes.POINTER(FseConfig), c_u8p, c_sz, c_u8p, c_sz,
+                                            ctypes.POINTER(c_sz)]),
+    ("zr_pazip_fse_removed_size", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(c_sz)]),
+    ("zr_pazip_fse_remove", ctypes.c_int32, [ctypes.POINTER(FseConfig), c_u8p, c_sz, c_u8p, c_sz,
+                                             ctypes.POINTER(c_sz)]),
+    ("zr_dictzip_entropy_encode", ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, c_vp, ctypes.c_float, c_u8p,
+                                                   c_sz, c_u8p, c_sz, ctypes.POINTER(c_sz), c_i32p]),
+    ("zr_dictzip_entropy_decode", ctypes.c_int32, [ctypes.c_int32, c_vp, c_u8p, c_sz, c_sz, c_u8p, c_sz,
+                                                   ctypes.POINTER(c_sz)]),
     ("zr_huff_tree_build", ctypes.c_int32, [c_u32p, ctypes.POINTER(HuffTree)]),
     ("zr_huff_encode_bound", c_sz, [ctypes.POINTER(HuffTree), c_sz]),
     ("zr_huff_encode", ctypes.c_int32, [ctypes.POINTER(HuffTree), c_u8p, c_sz, c_u8p, c_sz,

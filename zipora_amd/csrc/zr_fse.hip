@@ -1126,4 +1126,101 @@ int32_t zr_fse_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_
     ZR_GUARD_END
 }
 
+
+// ---- FSE as the PA-Zip second stage (dict_zip/compression_types.rs:2272-2340)
+// dict_zip's FseConfig maps to the entropy config with parallel_blocks None and
+// 64 KiB blocks/tables (compression_types.rs:2107-2123).
+static zr_fse_config pazip_cfg(const zr_fse_config *c) {
+    zr_fse_config e = *c;
+    e.parallel_blocks = 0;
+    e.block_size = 64 * 1024;
+    e.max_table_size = 64 * 1024;
+    return e;
+}
+
+size_t zr_pazip_fse_bound(size_t n, const zr_fse_config *c) {
+    const zr_fse_config e = pazip_cfg(c);
+    return 2 + std::max(n, zr_fse_compress_bound(n, &e));
+}
+
+// apply_fse_compression: "UN" | raw below 32 bytes or when FSE does not shrink
+// the data, else "FS" | FseCompressor::compress (a fresh encoder per call)
+int32_t zr_pazip_fse_apply(const zr_fse_config *c, const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                           size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!c || !out_len || (!in && n) || (!out && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    if (n == 0) return ZR_OK;
+    auto raw = [&]() -> int32_t {
+        if (out_cap < n + 2) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+        out[0] = 0x55;
+        out[1] = 0x4E;
+        memcpy(out + 2, in, n);
+        *out_len = n + 2;
+        return ZR_OK;
+    };
+    if (n < 32) return raw();
+    const zr_fse_config e = pazip_cfg(c);
+    int32_t st = fse_validate(&e);  // FseCompressor::with_config -> FseEncoder::new
+    if (st) return st;
+    std::vector<uint8_t> tmp(zr_fse_compress_bound(n, &e));
+    size_t cl = 0;
+    if ((st = zr_fse_compress(&e, in, n, tmp.data(), tmp.size(), &cl))) return st;
+    if (cl >= n) return raw();
+    if (out_cap < cl + 2) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+    out[0] = 0xFE;
+    out[1] = 0x53;
+    memcpy(out + 2, tmp.data(), cl);
+    *out_len = cl + 2;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_pazip_fse_removed_size(const uint8_t *in, size_t n, size_t *size) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!size || (!in && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *size = 0;
+    if (n < 2) {
+        *size = n;
+        return ZR_OK;
+    }
+    if (in[0] == 0x55 && in[1] == 0x4E) {
+        *size = n - 2;
+        return ZR_OK;
+    }
+    if (in[0] == 0xFE && in[1] == 0x53) return zr_fse_decompressed_size(in + 2, n - 2, size);
+    return zr_fse_decompressed_size(in, n, size);
+    ZR_GUARD_END
+}
+
+// remove_fse_compression: "UN" -> raw, "FS" -> FseCompressor::decompress, no
+// magic -> decompress the whole input (older format), < 2 bytes -> as is
+int32_t zr_pazip_fse_remove(const zr_fse_config *c, const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                            size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!c || !out_len || (!in && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    if (n == 0) return ZR_OK;
+    auto copy = [&](const uint8_t *p, size_t len) -> int32_t {
+        if (len > out_cap || (!out && len)) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+        if (len) memcpy(out, p, len);
+        *out_len = len;
+        return ZR_OK;
+    };
+    if (n < 2) return copy(in, n);
+    if (in[0] == 0x55 && in[1] == 0x4E) return copy(in + 2, n - 2);
+    const zr_fse_config e = pazip_cfg(c);
+    int32_t st = fse_validate(&e);
+    if (st) return st;
+    const bool fs = in[0] == 0xFE && in[1] == 0x53;
+    const uint8_t *p = fs ? in + 2 : in;
+    const size_t len = fs ? n - 2 : n;
+    if (len == 0) return ZR_OK;  // FseCompressor::decompress(&[]) -> empty
+    return zr_fse_decompress(p, len, out, out_cap, out_len);
+    ZR_GUARD_END
+}
+
 }  // extern "C"

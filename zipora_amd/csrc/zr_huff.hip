@@ -1266,4 +1266,85 @@ int32_t zr_ctx_huff_deserialize(const uint8_t *in, size_t n, zr_ctx_huff **out) 
     ZR_GUARD_END
 }
 
+
+// ---- DictZipBlobStore entropy stage (dict_zip/blob_store.rs:1075-1224)
+// algo: 0 None, 1 HuffmanO1 (model = ContextualHuffmanEncoder::new(dictionary,
+// Order1)), 2 Fse. The encoded form is kept only when encoded/raw (as f32)
+// <= ratio_require (check_compression_ratio, :1155-1161).
+int32_t zr_dictzip_entropy_encode(int32_t algo, int32_t interleave, const zr_ctx_huff *o1_model,
+                                  float ratio_require, const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                                  size_t *out_len, int32_t *algo_used) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!out_len || !algo_used || (!in && n) || (!out && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    *algo_used = 0;
+    auto raw = [&]() -> int32_t {
+        if (n > out_cap) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+        if (n) memcpy(out, in, n);
+        *out_len = n;
+        *algo_used = 0;
+        return ZR_OK;
+    };
+    if (algo == 0) return raw();
+    std::vector<uint8_t> enc;
+    size_t el = 0;
+    int32_t st;
+    if (algo == 1) {
+        if (!o1_model) return set_error(ZR_INVALID_INPUT, "HuffmanO1 needs the dictionary's order-1 model");
+        int nway;
+        switch (interleave) {  // apply_huffman_o1_encoding (:1114-1124)
+            case 0: case 1: nway = 1; break;
+            case 2: nway = 2; break;
+            case 4: nway = 4; break;
+            case 8: nway = 8; break;
+            default: return set_error(ZR_INVALID_INPUT, "Invalid interleaving factor");
+        }
+        enc.resize(zr_ctx_huff_encode_bound(o1_model, n) + 16);
+        st = zr_ctx_huff_encode(o1_model, nway, in, n, enc.data(), enc.size(), &el);
+    } else if (algo == 2) {  // apply_fse_encoding (:1128-1152)
+        zr_fse_config c;
+        zr_fse_config_default(&c);
+        c.parallel_blocks = interleave > 1 ? (uint64_t)interleave : 0;
+        enc.resize(zr_fse_compress_bound(n, &c));
+        st = zr_fse_compress(&c, in, n, enc.data(), enc.size(), &el);
+    } else {
+        return set_error(ZR_INVALID_INPUT, "unknown entropy algorithm");
+    }
+    if (st) return st;
+    if (n == 0 || !((float)el / (float)n <= ratio_require)) return raw();
+    if (el > out_cap) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+    memcpy(out, enc.data(), el);
+    *out_len = el;
+    *algo_used = algo;
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+// decode_entropy (:1164-1224). HuffmanO1 decodes with the non-interleaved
+// decoder and the record's original size, whatever the encode interleaving
+// was (:1179-1206) -- reproduced as is.
+int32_t zr_dictzip_entropy_decode(int32_t algo, const zr_ctx_huff *o1_model, const uint8_t *in, size_t n,
+                                  size_t original_size, uint8_t *out, size_t out_cap, size_t *out_len) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!out_len || (!in && n)) return set_error(ZR_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    if (algo == 0) {
+        if (n > out_cap || (!out && n)) return set_error(ZR_INVALID_INPUT, "output buffer too small");
+        if (n) memcpy(out, in, n);
+        *out_len = n;
+        return ZR_OK;
+    }
+    if (algo == 1) {
+        if (!o1_model) return set_error(ZR_INVALID_INPUT, "HuffmanO1 needs the dictionary's order-1 model");
+        if (original_size > out_cap || (!out && original_size))
+            return set_error(ZR_INVALID_INPUT, "output buffer too small");
+        return zr_ctx_huff_decode(o1_model, 0, in, n, out, original_size, out_len);
+    }
+    if (algo == 2) return zr_fse_decompress(in, n, out, out_cap, out_len);
+    return set_error(ZR_INVALID_INPUT, "unknown entropy algorithm");
+    ZR_GUARD_END
+}
+
 }  // extern "C"
