@@ -1382,7 +1382,9 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
     uint32_t xmin = 0xFFFFFFFFu;
     uint64_t acc = 0;
     uint32_t nacc = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0;
-    uint64_t nout = 0;  // bytes stored
+    uint64_t nout = 0;  // bytes stored (or staged in B0..B2)
+    x4u B0 = {0, 0, 0, 0}, B1 = B0, B2 = B0;
+    uint32_t npb = 0;  // staged 16-byte blocks
     auto enc_step = [&](const uint4 e) {  // rans.rs:303-335 (see k_enc_xn)
         xmin = min(xmin, e.x);
         const uint32_t nb = x >= e.y ? 16u : (x >= e.x ? 8u : 0u);
@@ -1402,7 +1404,24 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
             nacc -= 32;
             if (++nq == 4) {
                 if (vec_out) {
-                    *reinterpret_cast<x4u *>(out + nout) = x4u{q0, q1, q2, q3};
+                    // full 16-byte blocks wait in B0..B2 until a 64-byte boundary
+                    // of the output, then go out together: the record's lines
+                    // reach the L2 in 64-byte runs, not 16-byte pieces spread
+                    // over the kernel (written back as partial lines)
+                    const x4u blk = x4u{q0, q1, q2, q3};
+                    x4u *d = reinterpret_cast<x4u *>(out + nout);
+                    if ((((uintptr_t)(d + 1)) & 63) == 0) {
+                        if (npb >= 3) d[-3] = B0;
+                        if (npb >= 2) d[-2] = npb == 3 ? B1 : B0;
+                        if (npb >= 1) d[-1] = npb == 3 ? B2 : (npb == 2 ? B1 : B0);
+                        *d = blk;
+                        npb = 0;
+                    } else {
+                        B0 = npb == 0 ? blk : B0;
+                        B1 = npb == 1 ? blk : B1;
+                        B2 = npb == 2 ? blk : B2;
+                        npb++;
+                    }
                 } else {
                     const uint32_t qs[4] = {q0, q1, q2, q3};
                     for (int i = 0; i < 16; i++) out[nout + i] = (uint8_t)(qs[i >> 2] >> (8 * (i & 3)));
@@ -1445,7 +1464,13 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
             }
         }
     }
-    // drain: queued dwords, the partial dword, then the u64 state
+    // drain: staged blocks, queued dwords, the partial dword, then the u64 state
+    {
+        x4u *d = reinterpret_cast<x4u *>(out + nout);
+        if (npb >= 3) d[-3] = B0;
+        if (npb >= 2) d[-2] = npb == 3 ? B1 : B0;
+        if (npb >= 1) d[-1] = npb == 3 ? B2 : (npb == 2 ? B1 : B0);
+    }
     {
         const uint32_t qs[4] = {q0, q1, q2, q3};
         for (uint32_t i = 0; i < nq; i++) {
@@ -1551,6 +1576,173 @@ __global__ __launch_bounds__(256) void k_dec_x1_fast(const uint8_t *enc, uint8_t
         for (uint32_t t = 0; t < r; t++) out[g + 4 * cq + t] = (uint8_t)(acc >> (8 * (4 - r + t)));
     }
 }
+
+
+// per-lane x1 decode straight from global memory, 64-bit state (the fallback
+// of k_dec_x1_ring for non-standard states and single-symbol/empty tables)
+__device__ bool x1_dec_generic(const RansDTab *T, const uint32_t *stab, bool normal, const uint8_t *e,
+                               uint64_t len, uint64_t X, uint8_t *out, uint64_t n) {
+    uint64_t pos = len - 8;
+    for (uint64_t i = 0; i < n; i++) {
+        while (X < RANS_L) {  // rans.rs:479-485
+            if (pos == 0) return false;
+            X = (X << 8) | e[--pos];
+        }
+        uint32_t sy;
+        if (!normal) {
+            const uint32_t slot = (uint32_t)(X & (TOTFREQ - 1));
+            sy = T->slot[slot] & 0xFF;
+            X = (uint64_t)T->freq[sy] * (X >> TF_SHIFT) + slot - T->start[sy];
+        } else {
+            const uint32_t ent = stab[X & (TOTFREQ - 1)];
+            sy = ent & 0xFF;
+            X = (uint64_t)(ent >> 20) * (X >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
+        }
+        out[i] = (uint8_t)sy;
+    }
+    return true;
+}
+
+// x1 decode with a per-lane LDS byte ring (rans.rs:523-545 decode_single).
+// Each lane decodes one record. Its compressed bytes reach a private ring of
+// X1R 16-byte chunks ([dword row][lane] in LDS) by prefetches issued one
+// 16-symbol group ahead: a group consumes at most 32 bytes (two renorm bytes
+// per symbol), so landing the chunks down to 64 bytes below the read position
+// at every group boundary keeps each group's reads resident, and the loads'
+// latency overlaps a whole group instead of stalling the symbol that crosses
+// a chunk (k_dec_x1_fast: one exposed HBM load per symbol for a wave).
+// Lanes whose state is outside [L, 2^24), or tables other than DT_NORMAL, run
+// the generic per-lane loop.
+constexpr uint32_t X1W = 512;  // records per workgroup
+constexpr uint32_t X1R = 8;    // ring chunks per lane
+__global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t *raw, KArgs a) {
+    __shared__ uint32_t stab[TOTFREQ];
+    __shared__ uint32_t ring[X1R * 4 * X1W];
+    const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);
+    for (uint32_t j = threadIdx.x; j < TOTFREQ; j += X1W) stab[j] = T->slot[j];
+    const bool normal = T->kind == DT_NORMAL;
+    __syncthreads();
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b = blockIdx.x * X1W + tid;
+    if (b >= a.B) return;
+    const uint64_t n = a.len[b];
+    if (n == 0 || !single_mode(n, a.N)) return;
+    const uint64_t len = a.enc_len[b];
+    if (len < 8) {  // "rANS data too short" (rans.rs:524-526)
+        a.status[b] = ZR_INVALID_INPUT;
+        return;
+    }
+    const uint8_t *e = enc + a.enc_off[b];
+    const uint64_t X = ld_u64_u(e + len - 8);
+    uint8_t *out = raw + a.raw_off[b];
+    if (!normal || X < RANS_L || X >= (1ull << 24) || len >= (1ull << 31)) {
+        if (!x1_dec_generic(T, stab, normal, e, len, X, out, n)) a.status[b] = ZR_INVALID_INPUT;
+        return;
+    }
+    const x4u *e4 = reinterpret_cast<const x4u *>(e - (((uintptr_t)e) & 15));
+    uint64_t ab = (len - 8) + (((uintptr_t)e) & 15);  // e4-relative address of the first unread byte + 1
+    const uint64_t abmin = ((uintptr_t)e) & 15;      // bytes below abmin are not the record's
+    uint32_t *rl = ring + tid;
+    auto slot_of = [&](int64_t c) -> uint32_t * { return rl + (uint32_t)((c & (X1R - 1)) * 4) * X1W; };
+    auto land = [&](int64_t c, const x4u v) {
+        uint32_t *p = slot_of(c);
+        p[0] = v.x;
+        p[X1W] = v.y;
+        p[2 * X1W] = v.z;
+        p[3 * X1W] = v.w;
+    };
+    // initial fill: the 4 chunks below the read position
+    const int64_t ctop = ab ? (int64_t)((ab - 1) >> 4) : 0;
+    int64_t lowc = ctop;
+    for (int k = 0; k < 4; k++) {
+        const int64_t c = ctop - k;
+        if (c < 0) break;
+        land(c, e4[c]);
+        lowc = c;
+    }
+    x4u pf0 = {0, 0, 0, 0}, pf1 = pf0;
+    int64_t pfc = 0;
+    uint32_t pfn = 0;
+    uint32_t x = (uint32_t)X;
+    bool err = false;
+    // one decode step, branch-free. From a state in [16, 2^24) the renorm takes
+    // r1 = x < 2^16 and r2 = x < 2^8 bytes, known from x alone, so the two ring
+    // dwords holding bytes ab-1 and ab-2 are read before the shift is chosen:
+    // two LDS round trips per step (bytes, then the slot) instead of three.
+    // ia = ab as a signed 32-bit count (records < 2 GiB); reads below the
+    // record are harmless ring reads, and running out of data ("Insufficient
+    // data", rans.rs:480-482) shows as ia < abmin at the group's end.
+    int32_t ia = (int32_t)ab;
+    const int32_t iamin = (int32_t)abmin;
+    auto step = [&]() -> uint32_t {
+        const uint32_t q = (uint32_t)(ia - 2);  // the lower of the two candidate bytes
+        const uint32_t d = q >> 2;
+        const uint32_t lo = rl[(d & (4 * X1R - 1)) * X1W], hi = rl[((d + 1) & (4 * X1R - 1)) * X1W];
+        const uint32_t w16 = __builtin_amdgcn_alignbit(hi, lo, 8 * (q & 3)) & 0xFFFF;  // b1:b2
+        const bool r1 = x < RANS_L, r2 = x < 256;
+        x = r2 ? ((x << 16) | w16) : (r1 ? ((x << 8) | (w16 >> 8)) : x);
+        ia -= (r1 ? 1 : 0) + (r2 ? 1 : 0);
+        const uint32_t ent = stab[x & (TOTFREQ - 1)];
+        x = (ent >> 20) * (x >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
+        return ent & 0xFF;
+    };
+    const bool vec_out = (((uintptr_t)out) & 15) == 0;
+    const uint64_t nfull = vec_out ? n >> 4 : 0;  // 16-symbol groups stored as 16-byte words
+    uint64_t g = 0;
+    // one 16-symbol group: land the chunks prefetched at the previous
+    // boundary, prefetch the next ones, decode into o[0..3]
+    auto group = [&](uint32_t *o) {
+        if (pfn >= 1) land(pfc, pf0);
+        if (pfn >= 2) land(pfc - 1, pf1);
+        if (pfn) lowc = pfc - (int64_t)pfn + 1;
+        const int64_t target = ia >= 64 ? (int64_t)((ia - 64) >> 4) : 0;
+        const int64_t want = lowc - (target > 0 ? target : 0);
+        pfn = want <= 0 ? 0u : (want >= 2 ? 2u : 1u);
+        if (lowc - (int64_t)pfn < 0) pfn = (uint32_t)lowc;
+        pfc = lowc - 1;
+        pf0 = e4[pfn >= 1 ? pfc : ctop];
+        pf1 = e4[pfn >= 2 ? pfc - 1 : ctop];
+        o[0] = o[1] = o[2] = o[3] = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) o[k >> 2] |= step() << (8 * (k & 3));
+    };
+    // eight groups per 128-byte store: a record's output lines are written
+    // whole, not in 16-byte pieces spread over the kernel (the L2 wrote the
+    // partial lines back: 2.47 -> 1.57 ms with 64-byte stores)
+    for (; g + 8 <= nfull && !err; g += 8) {
+        uint32_t o[32];
+#pragma unroll
+        for (int k = 0; k < 8; k++) group(o + 4 * k);
+        err = ia < iamin;
+        x4u *d = reinterpret_cast<x4u *>(out + 16 * g);
+#pragma unroll
+        for (int k = 0; k < 8; k++) d[k] = x4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+    }
+    for (; g < nfull && !err; g++) {
+        uint32_t o[4];
+        group(o);
+        err = ia < iamin;
+        *reinterpret_cast<x4u *>(out + 16 * g) = x4u{o[0], o[1], o[2], o[3]};
+    }
+    if (!err && g < (n + 15) >> 4) {  // tail (or an unaligned output): land, then byte stores
+        if (pfn >= 1) land(pfc, pf0);
+        if (pfn >= 2) land(pfc - 1, pf1);
+        if (pfn) lowc = pfc - (int64_t)pfn + 1;
+        for (uint64_t i = 16 * g; i < n && !err; i++) {
+            if ((i & 15) == 0) {  // keep 64 bytes below the read position resident
+                const int64_t target = ia >= 64 ? (int64_t)((ia - 64) >> 4) : 0;
+                while (lowc > 0 && lowc > target) {
+                    lowc--;
+                    land(lowc, e4[lowc]);
+                }
+            }
+            out[i] = (uint8_t)step();
+            err = ia < iamin;
+        }
+    }
+    if (err) a.status[b] = ZR_INVALID_INPUT;
+}
+
 
 // ======================================================================
 // host launchers
@@ -1734,7 +1926,7 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
     timer_begin("rans_decode_x1", s);
     if (!(bt->min_len >= a.N && a.N > 1)) {
         if (a.table_stride == 0)
-            hipLaunchKernelGGL(k_dec_x1_fast, dim3((uint32_t)ceil_div(a.B, 256)), dim3(256), 0, s, enc, raw, a);
+            hipLaunchKernelGGL(k_dec_x1_ring, dim3((uint32_t)ceil_div(a.B, X1W)), dim3(X1W), 0, s, enc, raw, a);
         else
             hipLaunchKernelGGL(k_dec_x1_generic, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, enc, raw, a);
     }
