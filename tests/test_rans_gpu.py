@@ -245,3 +245,32 @@ def test_rans_host_pipe_errors(zr, oracle):
     st = pipe.decode([100, 100], enc, enc_off, enc_len2, out, raw_off)
     assert st[0] == 0 and st[1] != 0
     assert bytes(out[:100].numpy()) == b"a" * 100
+
+
+@pytest.mark.parametrize("align", [16, 1])
+def test_shared_histogram_small_records(zr, align):
+    """Shared histogram of many <= 1 KiB records (the blob-store path): equals the
+    byte counts of the records' concatenation (rans.rs:708-714 caller semantics)."""
+    import numpy as np
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    rnd = random.Random(align)
+    lens = [rnd.choice([0, 1, 15, 16, 17, 255, 1000, 1023, 1024]) for _ in range(1000)] + [1024] * 200
+    bt = RansDeviceBatch(lens, 1, shared_table=True, align=align)
+    raw = bt.new_raw()
+    datas = []
+    for b, n in enumerate(lens):
+        d = zr.synth("z" if b % 2 else "u", n, seed=b)
+        datas.append(d)
+        o = bt.raw_off_host[b]
+        if n:
+            raw[o:o + n] = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+    # bytes outside the records must not be counted
+    gaps = torch.ones_like(raw, dtype=torch.bool)
+    for b, n in enumerate(lens):
+        gaps[bt.raw_off_host[b]:bt.raw_off_host[b] + n] = False
+    raw[gaps] = 0xAB
+    bt.histogram(raw)
+    torch.cuda.synchronize()
+    want = np.bincount(np.frombuffer(b"".join(datas), dtype=np.uint8), minlength=256)
+    assert bt.hist[:256].cpu().numpy().astype(np.int64).tolist() == want.tolist()

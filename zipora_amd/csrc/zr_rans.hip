@@ -165,6 +165,59 @@ __global__ __launch_bounds__(256) void k_hist(const uint8_t *raw, KArgs a, int s
     }
 }
 
+// Shared histogram of many small buffers (every len <= 1024, e.g. blob-store
+// records): a wave takes 64 consecutive buffers, reads their offsets and
+// lengths with one coalesced load, then covers four buffers per round with one
+// 16-byte load per lane each (lane l: bytes 16l..16l+15), so four loads are in
+// flight instead of k_hist's two dependent metadata loads per 1 KiB item.
+__global__ __launch_bounds__(256) void k_hist_small(const uint8_t *raw, KArgs a, uint32_t *hist) {
+    __shared__ uint32_t h[256 * HCOPY];
+    for (int i = threadIdx.x; i < 256 * HCOPY; i += 256) h[i] = 0;
+    __syncthreads();
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63, cp = threadIdx.x & (HCOPY - 1);
+    const uint32_t ngroups = (a.B + 63) / 64;
+    for (uint32_t g = blockIdx.x * 4 + wv; g < ngroups; g += gridDim.x * 4) {
+        const uint32_t mb = g * 64 + lane;
+        const uint32_t L = mb < a.B ? (uint32_t)a.len[mb] : 0u;
+        const uint64_t O = mb < a.B ? a.raw_off[mb] : 0;
+        const uint32_t Olo = (uint32_t)O, Ohi = (uint32_t)(O >> 32);
+        for (uint32_t j = 0; j < 64; j += 4) {
+            v4u v[4];
+            uint32_t nv[4];
+            bool full[4];
+            const uint8_t *pp[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t Lk = __shfl(L, j + k, 64);
+                const uint64_t Ok = (uint64_t)(uint32_t)__shfl(Olo, j + k, 64) |
+                                    ((uint64_t)(uint32_t)__shfl(Ohi, j + k, 64) << 32);
+                const uint32_t lo = 16 * lane;
+                nv[k] = lo < Lk ? min(16u, Lk - lo) : 0u;
+                pp[k] = raw + Ok + lo;
+                full[k] = nv[k] == 16 && (((uintptr_t)pp[k]) & 15) == 0;
+                v[k] = full[k] ? __builtin_nontemporal_load(reinterpret_cast<const v4u *>(pp[k])) : v4u{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (full[k]) {
+                    hist_add4(h, v[k].x, cp);
+                    hist_add4(h, v[k].y, cp);
+                    hist_add4(h, v[k].z, cp);
+                    hist_add4(h, v[k].w, cp);
+                } else {
+                    for (uint32_t t = 0; t < nv[k]; t++) atomicAdd(&h[((uint32_t)pp[k][t] << 5) + cp], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t v = threadIdx.x;
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t k = 0; k < HCOPY; k++) sum += h[(v << 5) + ((k + v) & (HCOPY - 1))];
+    if (sum) atomicAdd(&hist[v], sum);
+}
+
 // ======================================================================
 // table build on device: Rans64Encoder::new (rans.rs:208-235) with
 // normalize_frequencies (rans.rs:238-299) and the symbol starts (rans.rs:225-228)
@@ -1826,8 +1879,13 @@ int32_t zr_histogram_dev(const uint8_t *raw, const zr_rans_batch *bt, int32_t sh
     // shared: 5 resident 32-KiB-LDS workgroups per CU on 256 CUs, 4 waves each
     const uint64_t grid = shared ? std::min<uint64_t>(ceil_div(items, 4), 1280) : items;
     timer_begin("histogram", (hipStream_t)stream);
-    hipLaunchKernelGGL(k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a,
-                       shared, hist_dev, chunk, nchunk);
+    if (shared && bt->max_len <= 1024 && a.B >= 64) {  // many small buffers: blob-store records
+        const uint64_t g2 = std::min<uint64_t>(ceil_div(ceil_div(a.B, 64), 4), 1280);
+        hipLaunchKernelGGL(k_hist_small, dim3((uint32_t)g2), dim3(256), 0, (hipStream_t)stream, raw, a, hist_dev);
+    } else {
+        hipLaunchKernelGGL(k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a,
+                           shared, hist_dev, chunk, nchunk);
+    }
     timer_end("histogram", (hipStream_t)stream);
     ZR_HIP(hipGetLastError());
     return ZR_OK;
