@@ -755,6 +755,21 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
         x |= (x == 0) ? 1u : 0u;  // x = max(x, 1)
         return e & 0xFF;
     };
+    // a group that starts with >= 68 unread bytes never reaches the stream's
+    // last 1..3 bytes (one word per step at most): renormalise without that
+    // branch, and with max(x, 1) folded into the word merge (after a word
+    // merge x is 0 only when the decoded x and the word both are)
+    auto step_bulk = [&]() -> uint32_t {
+        const uint32_t e = s_slot[x & 4095];
+        const uint64_t xd = (uint64_t)(((e >> 8) & 4095) + 1) * (x >> 12) + (e >> 20);
+        const bool small = xd < 65536;
+        const uint64_t merged = (xd << 32) | nw | ((xd == 0 && nw == 0) ? 1u : 0u);
+        x = small ? merged : xd;
+        bp -= small ? 4 : 0;
+        m -= small ? 1 : 0;
+        nw = read_word(m);
+        return e & 0xFF;
+    };
     const uint32_t G = fast ? (uint32_t)(B.orig >> 4) : 0u;
     const bool vec = (((uintptr_t)out) & 15) == 0;
     uint32_t Gmax = vec ? G : 0u;  // unaligned output: everything in the tail loop
@@ -788,8 +803,13 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
     auto group = [&](uint32_t g) {
         if (g < Gl) {
             uint32_t o[4] = {0, 0, 0, 0};
+            if (bp >= 68) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) o[k >> 2] |= step() << (8 * (k & 3));
+                for (int k = 0; k < 16; k++) o[k >> 2] |= step_bulk() << (8 * (k & 3));
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; k++) o[k >> 2] |= step() << (8 * (k & 3));
+            }
             o4[g] = fv4u{o[0], o[1], o[2], o[3]};
         }
     };
