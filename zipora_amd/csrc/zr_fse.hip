@@ -254,18 +254,20 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
     auto step_e = [&](const uint4 e) {
         const uint32_t f = e.w & 0xFFFF;
         err |= (f == 0);  // encode_symbol returns None (fse.rs:946-953)
-        // renormalize_encode: x_max = ((RANS_L >> 12) << 32) * freq = freq << 36
-        if (x >= ((uint64_t)(f ? f : 1u) << 36)) {
-            q0 = q1;
-            q1 = q2;
-            q2 = q3;
-            q3 = (uint32_t)x;
-            x >>= 32;
-            if (++nq == 4) {
-                out4[nout >> 2] = fv4u{q0, q1, q2, q3};
-                nout += 4;
-                nq = 0;
-            }
+        // renormalize_encode: x_max = ((RANS_L >> 12) << 32) * freq = freq << 36.
+        // The word shift is branch-free (selects); only the 16-byte store of a
+        // full queue branches, once per four words.
+        const bool emit = x >= ((uint64_t)(f ? f : 1u) << 36);
+        q0 = emit ? q1 : q0;
+        q1 = emit ? q2 : q1;
+        q2 = emit ? q3 : q2;
+        q3 = emit ? (uint32_t)x : q3;
+        x = emit ? (x >> 32) : x;
+        nq += emit ? 1 : 0;
+        if (nq == 4) {
+            out4[nout >> 2] = fv4u{q0, q1, q2, q3};
+            nout += 4;
+            nq = 0;
         }
         const uint64_t rcp = ((uint64_t)e.y << 32) | e.x;
         const uint64_t q = mul_hi_portable(x, rcp) >> (e.w >> 16);
