@@ -7,4 +7,5 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_rans.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --workload fse > gpurun_out/bench_fse.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --workload o1 > gpurun_out/bench_o1.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --workload blob > gpurun_out/bench_blob.log 2>&1
+timeout -k 10 300 python -u bench.py --workload blob > gpurun_out/bench_blob.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --workload fse --fse-block-kib 16 --no-cpu-baseline > gpurun_out/bench_fse16.log 2>&1
