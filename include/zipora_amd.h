@@ -155,6 +155,14 @@ int32_t zr_rans_pipe_destroy(zr_rans_pipe *pipe);
 int32_t zr_rans_pipe_encode(zr_rans_pipe *pipe, uint32_t n_buffers, const uint64_t *len,
                             const uint8_t *raw, const uint64_t *raw_off, uint8_t *enc,
                             const uint64_t *enc_off, uint64_t *enc_len, int32_t *status);
+/* encode into a packed host layout (records back to back, the ZipOffset
+ * content area): enc_off[b] and enc_len[b] are outputs, enc_total the bytes
+ * written; enc_cap >= the sum of zr_rans_encode_bound(len[b]). Only the
+ * encoded bytes cross PCIe. Failed buffers get status != 0 and length 0. */
+int32_t zr_rans_pipe_encode_packed(zr_rans_pipe *pipe, uint32_t n_buffers, const uint64_t *len,
+                                   const uint8_t *raw, const uint64_t *raw_off, uint8_t *enc,
+                                   size_t enc_cap, uint64_t *enc_off, uint64_t *enc_len,
+                                   int32_t *status, uint64_t *enc_total);
 int32_t zr_rans_pipe_decode(zr_rans_pipe *pipe, uint32_t n_buffers, const uint64_t *len,
                             const uint8_t *enc, const uint64_t *enc_off, const uint64_t *enc_len,
                             uint8_t *raw, const uint64_t *raw_off, int32_t *status);

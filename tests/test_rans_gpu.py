@@ -214,6 +214,43 @@ def _pipe_roundtrip(zr, oracle, lens, N, kind, group_bytes, pinned=True):
     pipe.close()
 
 
+def test_rans_host_pipe_packed(zr, oracle):
+    """Packed encode: records back to back (offsets = exclusive scan of lengths),
+    bytes equal the oracle's; decode from the packed layout restores the input."""
+    import numpy as np
+    import torch
+    from zipora_amd.device import RansHostPipe
+    for lens, N, kind, group in (([1024] * 3000 + [0, 17, 5], 1, "t", 256 << 10),
+                                 ([300000, 0, 5, 70000, 1 << 20, 4096], 4096, "u", 512 << 10)):
+        datas = [zr.synth(kind, n, seed=500 + b) for b, n in enumerate(lens)]
+        freqs = oracle.histogram(b"".join(datas))
+        pipe = RansHostPipe(zr.Rans64Encoder(freqs, N).table, N, group)
+        raw_off, _, rb, eb = pipe.layout(lens)
+        raw = torch.zeros(max(rb, 1), dtype=torch.uint8, pin_memory=True)
+        for b, d in enumerate(datas):
+            o = int(raw_off[b])
+            if d:
+                raw[o:o + len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8)
+        enc = torch.zeros(max(eb, 1), dtype=torch.uint8, pin_memory=True)
+        enc_off, enc_len, st, total = pipe.encode_packed(lens, raw, raw_off, enc)
+        assert (st == 0).all()
+        assert total == int(enc_len.sum())
+        assert enc_off.tolist() == (np.concatenate([[0], np.cumsum(enc_len)[:-1]]).tolist() if len(lens) else [])
+        t = oracle.rans_table(freqs)
+        encb = enc.numpy()
+        for b, d in enumerate(datas):
+            o = int(enc_off[b])
+            assert encb[o:o + int(enc_len[b])].tobytes() == oracle.rans_encode(t, N, d), f"buffer {b}"
+        out = torch.zeros_like(raw)
+        st = pipe.decode(lens, enc, enc_off, enc_len, out, raw_off)
+        assert (st == 0).all()
+        outb = out.numpy()
+        for b, d in enumerate(datas):
+            o = int(raw_off[b])
+            assert outb[o:o + len(d)].tobytes() == d
+        pipe.close()
+
+
 def test_rans_host_pipe(zr, oracle):
     # several groups per call (both slots reused), a buffer larger than a group,
     # empty and tiny buffers, pageable memory

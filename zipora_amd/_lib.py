@@ -76,6 +76,8 @@ SIGNATURES = [
     ("zr_rans_pipe_destroy", ctypes.c_int32, [c_vp]),
     ("zr_rans_pipe_encode", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                              c_vp]),
+    ("zr_rans_pipe_encode_packed", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp,
+                                                    c_vp, c_vp, c_vp]),
     ("zr_rans_pipe_decode", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                              c_vp]),
     ("zr_rans_compressor_train", ctypes.c_int32, [c_u8p, c_sz, ctypes.POINTER(RansTable)]),

@@ -35,6 +35,10 @@ struct Slot {
     size_t raw_cap = 0, enc_cap = 0;
     void *ws = nullptr;
     size_t ws_cap = 0;
+    uint8_t *pack = nullptr;    // packed encode output (device)
+    size_t pack_cap = 0;
+    void *poff = nullptr;       // packed offsets (device)
+    size_t poff_cap = 0;
     uint64_t *meta = nullptr;   // device: len | raw_off | enc_off | enc_len, then int32 status
     uint64_t *hmeta = nullptr;  // pinned host mirror
     uint64_t *hmeta_dev = nullptr;  // its device-side address
@@ -52,6 +56,47 @@ size_t meta_bytes(uint32_t nb) { return (size_t)nb * 4 * 8 + round_up((size_t)nb
 // serialise the copy streams.
 __global__ void k_words(const uint64_t *__restrict__ src, uint64_t *__restrict__ dst, uint32_t n) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
+// Packed encode output (records back to back, the ZipOffset content layout:
+// offsets = exclusive scan of the lengths): the group's exclusive scan of the
+// encoded lengths (failed buffers count 0), then one wave per buffer moves its
+// bytes from the bound-sized slot to the packed position.
+__global__ __launch_bounds__(1024) void k_pack_scan(const uint64_t *enc_len, const int32_t *status, uint32_t nb,
+                                                    uint64_t *poff) {
+    __shared__ unsigned long long wsum[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    unsigned long long carry = 0;
+    for (uint32_t base = 0; base < nb; base += 1024) {
+        const uint32_t i = base + tid;
+        const unsigned long long v = (i < nb && status[i] == 0) ? enc_len[i] : 0;
+        unsigned long long inc = v;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const unsigned long long t = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += t;
+        }
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        unsigned long long before = 0, total = 0;
+        for (uint32_t w = 0; w < 16; w++) {
+            before += w < wv ? wsum[w] : 0;
+            total += wsum[w];
+        }
+        if (i < nb) poff[i] = carry + before + inc - v;
+        carry += total;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pack_copy(const uint8_t *src, const uint64_t *slot_off,
+                                                   const uint64_t *enc_len, const int32_t *status,
+                                                   const uint64_t *poff, uint8_t *dst, uint32_t nb) {
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= nb || status[i] != 0) return;
+    const uint64_t L = enc_len[i];
+    const uint8_t *sp = src + slot_off[i];
+    uint8_t *dp = dst + poff[i];
+    for (uint64_t k = lane; k < L; k += 64) dp[k] = sp[k];
 }
 
 int32_t copy_words(const uint64_t *src, uint64_t *dst, size_t n, hipStream_t s) {
@@ -190,23 +235,64 @@ int32_t copy_extents(uint8_t *dst, const uint8_t *src, const std::vector<std::pa
 // One direction of the pipeline. Group g's input copy and coding are issued,
 // then group g-1's copy back (encode first waits for g-1's coding on the host:
 // only then are its encoded lengths, and so the extents to copy, known).
+// packed encode: the caller gets enc_off back (records back to back from 0)
+struct Packed {
+    bool on = false;
+    size_t cap = 0;
+    uint64_t *off_out = nullptr;
+    uint64_t pos = 0;
+};
+
 int32_t run(zr_rans_pipe *p, bool encode, uint32_t B, const uint64_t *len, uint8_t *raw,
             const uint64_t *raw_off, uint8_t *enc, const uint64_t *enc_off, uint64_t *enc_len,
-            int32_t *status) {
+            int32_t *status, Packed *pk = nullptr) {
     const uint32_t N = p->N;
     const auto gs = groups(len, B, p->group_cap);
     Trace tr;
     std::vector<uint64_t> bound(encode ? B : 0);
     for (uint32_t b = 0; b < (encode ? B : 0); b++) bound[b] = zr_rans_encode_bound(len[b], N);
+    const bool packed = pk && pk->on;
+    std::vector<uint64_t> slots;  // packed: the device slot layout (16-byte aligned bound slots)
+    if (packed) {
+        slots.resize(B);
+        uint64_t o = 0;
+        for (uint32_t b = 0; b < B; b++) {
+            slots[b] = o;
+            o += round_up(bound[b], 16);
+        }
+        enc_off = slots.data();
+    }
     const uint64_t *enc_n = encode ? bound.data() : enc_len;  // encoded extent per buffer, device side
     std::vector<uint64_t> rbase(gs.size()), ebase(gs.size());
+    std::vector<uint8_t> use_pack(gs.size(), 0);  // packed groups of small records: device packing
 
     auto issue_out = [&](size_t gi) -> int32_t {
         Slot &S = p->slot[gi & 1];
         const uint32_t b0 = gs[gi].first, b1 = gs[gi].second, nb = b1 - b0;
         ZR_HIP(hipStreamWaitEvent(p->s_out, S.code_done, 0));
         tr.mark(gi, 4, p->s_out);
-        if (encode) {
+        if (encode && packed) {
+            ZR_HIP(hipEventSynchronize(S.code_done));
+            const uint64_t *el = S.hmeta + 3 * (size_t)nb;
+            const int32_t *stt = reinterpret_cast<const int32_t *>(S.hmeta + 4 * (size_t)nb);
+            uint64_t tot = 0;
+            for (uint32_t i = 0; i < nb; i++) {
+                pk->off_out[b0 + i] = pk->pos + tot;
+                tot += stt[i] == 0 ? el[i] : 0;
+            }
+            if (pk->pos + tot > pk->cap) return set_error(ZR_INVALID_INPUT, "packed output buffer too small");
+            if (use_pack[gi]) {
+                if (tot) ZR_HIP(hipMemcpyAsync(enc + pk->pos, S.pack, tot, hipMemcpyDeviceToHost, p->s_out));
+            } else {  // large records: each straight from its slot to its packed place
+                for (uint32_t i = 0; i < nb; i++) {
+                    const uint64_t L = stt[i] == 0 ? el[i] : 0;
+                    if (L)
+                        ZR_HIP(hipMemcpyAsync(enc + pk->off_out[b0 + i], S.enc + (enc_off[b0 + i] - ebase[gi]), L,
+                                              hipMemcpyDeviceToHost, p->s_out));
+                }
+            }
+            pk->pos += tot;
+        } else if (encode) {
             ZR_HIP(hipEventSynchronize(S.code_done));
             const uint64_t *el = S.hmeta + 3 * (size_t)nb;
             std::vector<uint64_t> off(nb), n(nb);
@@ -292,6 +378,19 @@ int32_t run(zr_rans_pipe *p, bool encode, uint32_t B, const uint64_t *len, uint8
         if ((st = copy_words(S.meta + 3 * (size_t)nb, S.hmeta_dev + 3 * (size_t)nb,
                              meta_bytes(nb) / 8 - 3 * (size_t)nb, p->s_cmp)))
             return st;
+        use_pack[gi] = packed && max_len <= (64u << 10);
+        if (use_pack[gi]) {  // small records: back to back in S.pack (group-relative offsets)
+            if ((st = grow(reinterpret_cast<void **>(&S.pack), &S.pack_cap, std::max<uint64_t>(ee - eb, 16))))
+                return st;
+            if ((st = grow(&S.poff, &S.poff_cap, 8 * (size_t)nb))) return st;
+            const int32_t *dst = reinterpret_cast<const int32_t *>(S.meta + 4 * (size_t)nb);
+            hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(1024), 0, p->s_cmp, S.meta + 3 * (size_t)nb, dst, nb,
+                               reinterpret_cast<uint64_t *>(S.poff));
+            hipLaunchKernelGGL(k_pack_copy, dim3((nb + 3) / 4), dim3(256), 0, p->s_cmp, S.enc, S.meta + 2 * (size_t)nb,
+                               S.meta + 3 * (size_t)nb, dst, reinterpret_cast<const uint64_t *>(S.poff), S.pack,
+                               nb);
+            ZR_HIP(hipGetLastError());
+        }
         tr.mark(gi, 3, p->s_cmp);
         ZR_HIP(hipEventRecord(S.code_done, p->s_cmp));
         S.busy = true;
@@ -319,6 +418,8 @@ void release(zr_rans_pipe *p) {
         if (S.ws) (void)hipFree(S.ws);
         if (S.meta) (void)hipFree(S.meta);
         if (S.hmeta) (void)hipHostFree(S.hmeta);
+        if (S.pack) (void)hipFree(S.pack);
+        if (S.poff) (void)hipFree(S.poff);
         if (S.in_done) (void)hipEventDestroy(S.in_done);
         if (S.code_done) (void)hipEventDestroy(S.code_done);
         if (S.out_done) (void)hipEventDestroy(S.out_done);
@@ -382,6 +483,27 @@ int32_t zr_rans_pipe_encode(zr_rans_pipe *p, uint32_t n_buffers, const uint64_t 
     if (!p || (n_buffers && (!len || !raw || !raw_off || !enc || !enc_off || !enc_len || !status)))
         return set_error(ZR_INVALID_INPUT, "null argument");
     return run(p, true, n_buffers, len, const_cast<uint8_t *>(raw), raw_off, enc, enc_off, enc_len, status);
+    ZR_GUARD_END
+}
+
+int32_t zr_rans_pipe_encode_packed(zr_rans_pipe *p, uint32_t n_buffers, const uint64_t *len, const uint8_t *raw,
+                                   const uint64_t *raw_off, uint8_t *enc, size_t enc_cap, uint64_t *enc_off,
+                                   uint64_t *enc_len, int32_t *status, uint64_t *enc_total) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!p || !enc_total ||
+        (n_buffers && (!len || !raw || !raw_off || !enc || !enc_off || !enc_len || !status)))
+        return set_error(ZR_INVALID_INPUT, "null argument");
+    Packed pk;
+    pk.on = true;
+    pk.cap = enc_cap;
+    pk.off_out = enc_off;
+    int32_t st = run(p, true, n_buffers, len, const_cast<uint8_t *>(raw), raw_off, enc, nullptr, enc_len, status, &pk);
+    *enc_total = pk.pos;
+    if (!st)  // failed buffers hold no bytes in the packed layout
+        for (uint32_t b = 0; b < n_buffers; b++)
+            if (status[b] != 0) enc_len[b] = 0;
+    return st;
     ZR_GUARD_END
 }
 

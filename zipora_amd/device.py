@@ -185,6 +185,22 @@ class RansHostPipe:
                                          self._p(enc_len), self._p(status)))
         return enc_len, status
 
+    def encode_packed(self, lens, raw, raw_off, enc):
+        """Records back to back in enc -> (enc_off, enc_len, status, total)."""
+        np = self._np
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        B = len(lens)
+        enc_off = np.zeros(B, dtype=np.uint64)
+        enc_len = np.zeros(B, dtype=np.uint64)
+        status = np.zeros(B, dtype=np.int32)
+        total = ctypes.c_uint64(0)
+        cap = enc.numel() if isinstance(enc, torch.Tensor) else enc.nbytes
+        check(self.L.zr_rans_pipe_encode_packed(self.h, B, self._p(lens), self._p(raw),
+                                                self._p(np.ascontiguousarray(raw_off, dtype=np.uint64)),
+                                                self._p(enc), cap, self._p(enc_off), self._p(enc_len),
+                                                self._p(status), ctypes.byref(total)))
+        return enc_off, enc_len, status, total.value
+
     def decode(self, lens, enc, enc_off, enc_len, raw, raw_off):
         """-> status numpy array."""
         np = self._np
