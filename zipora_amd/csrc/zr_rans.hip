@@ -1539,96 +1539,6 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
     a.enc_len[b] = nout + 8;
 }
 
-// rans.rs:523-560 decode_single: state = last 8 bytes; renormalisation bytes
-// are read backwards from len - 8 through a 16-byte register window
-__global__ __launch_bounds__(256) void k_dec_x1_fast(const uint8_t *enc, uint8_t *raw, KArgs a) {
-    __shared__ uint32_t stab[TOTFREQ];
-    const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);
-    for (uint32_t j = threadIdx.x; j < TOTFREQ; j += 256) stab[j] = T->slot[j];
-    const bool single = T->kind != DT_NORMAL;  // single-symbol / empty tables: global reads
-    __syncthreads();
-    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= a.B) return;
-    const uint64_t n = a.len[b];
-    if (n == 0 || !single_mode(n, a.N)) return;
-    const uint64_t len = a.enc_len[b];
-    if (len < 8) {  // "rANS data too short" (rans.rs:524-526)
-        a.status[b] = ZR_INVALID_INPUT;
-        return;
-    }
-    const uint8_t *e = enc + a.enc_off[b];
-    uint64_t X = ld_u64_u(e + len - 8);
-    uint64_t pos = len - 8;  // bytes [0, pos) unread
-    // backward byte reader: chunk cur holds the aligned 16 bytes containing pos - 1
-    const x4u *e4 = reinterpret_cast<const x4u *>(e - (((uintptr_t)e) & 15));
-    const uint64_t ebias = ((uintptr_t)e) & 15;  // e[i] = bytes of e4 at ebias + i
-    int64_t cidx = ((int64_t)(pos + ebias) - 1) >> 4;
-    x4u cur = {0, 0, 0, 0};
-    if (pos) cur = e4[cidx];
-    auto rd = [&]() -> uint32_t {  // pos > 0: return e[--pos]
-        pos--;
-        const uint64_t ab = pos + ebias;
-        const int64_t ci = (int64_t)(ab >> 4);
-        if (ci != cidx) {
-            cidx = ci;
-            cur = e4[ci];
-        }
-        const uint32_t k = (uint32_t)(ab & 15);
-        const uint32_t dw = (k >> 2) == 0 ? cur.x : (k >> 2) == 1 ? cur.y : (k >> 2) == 2 ? cur.z : cur.w;
-        return (dw >> (8 * (k & 3))) & 0xFF;
-    };
-    uint8_t *out = raw + a.raw_off[b];
-    const bool vec_out = (((uintptr_t)out) & 15) == 0;
-    uint32_t w0 = 0, w1 = 0, w2 = 0, acc = 0;
-    bool err = false;
-    uint64_t i = 0;
-    for (; i < n; i++) {
-        // renormalise first (rans.rs:479-485)
-        while (X < RANS_L) {
-            if (pos == 0) {
-                err = true;
-                break;
-            }
-            X = (X << 8) | rd();
-        }
-        if (err) break;
-        uint32_t sy;
-        if (single) {
-            const uint32_t slot = (uint32_t)(X & (TOTFREQ - 1));
-            sy = T->slot[slot] & 0xFF;
-            X = (uint64_t)T->freq[sy] * (X >> TF_SHIFT) + slot - T->start[sy];
-        } else {
-            const uint32_t ent = stab[X & (TOTFREQ - 1)];
-            sy = ent & 0xFF;
-            X = (uint64_t)(ent >> 20) * (X >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
-        }
-        if (vec_out) {
-            acc = (acc >> 8) | (sy << 24);
-            if ((i & 15) == 15) {
-                *reinterpret_cast<x4u *>(out + i - 15) = x4u{w0, w1, w2, acc};
-            } else if ((i & 3) == 3) {
-                w0 = w1;
-                w1 = w2;
-                w2 = acc;
-            }
-        } else {
-            out[i] = (uint8_t)sy;
-        }
-    }
-    if (err) {
-        a.status[b] = ZR_INVALID_INPUT;  // "Insufficient data" (rans.rs:480-482)
-        return;
-    }
-    const uint32_t rem = (uint32_t)(n & 15);
-    if (vec_out && rem) {
-        const uint64_t g = n - rem;
-        const uint32_t cq = rem >> 2, r = rem & 3;
-        const uint32_t ws[3] = {w0, w1, w2};
-        for (uint32_t k = 0; k < cq; k++)
-            for (int t = 0; t < 4; t++) out[g + 4 * k + t] = (uint8_t)(ws[3 - cq + k] >> (8 * t));
-        for (uint32_t t = 0; t < r; t++) out[g + 4 * cq + t] = (uint8_t)(acc >> (8 * (4 - r + t)));
-    }
-}
 
 
 // per-lane x1 decode straight from global memory, 64-bit state (the fallback
@@ -1663,7 +1573,7 @@ __device__ bool x1_dec_generic(const RansDTab *T, const uint32_t *stab, bool nor
 // per symbol), so landing the chunks down to 64 bytes below the read position
 // at every group boundary keeps each group's reads resident, and the loads'
 // latency overlaps a whole group instead of stalling the symbol that crosses
-// a chunk (k_dec_x1_fast: one exposed HBM load per symbol for a wave).
+// a chunk (the previous decoder: one exposed HBM load per symbol for a wave).
 // Lanes whose state is outside [L, 2^24), or tables other than DT_NORMAL, run
 // the generic per-lane loop.
 constexpr uint32_t X1W = 512;  // records per workgroup
