@@ -1306,7 +1306,7 @@ __global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t
             uint32_t hA, lA, sA, hB, lB, sB;
             const uint32_t eA = step(D, hA, lA, sA);
             const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
-            pos8 = pos8 + 16 - sA - sB;
+            pos8 -= sA + sB - 16u;  // (v_add3 + v_sub)
             if (j + 1 < DT2 / 2) D = readD(pos8);
             if (ABL & 1) {
                 sink += eA ^ eB;
