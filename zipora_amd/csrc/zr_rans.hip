@@ -378,16 +378,21 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
     if (single_mode(n, N)) return;
-    // per symbol: x = xmax = freq << 12 (0 = not in table), y = xmax << 8 (two
-    // renorm bytes at or above it), z = reciprocal,
-    // w = start | (4096 - freq) << 12 | rsh << 24
+    // The state is kept as X = x << 8 | g, g < 256 an arbitrary low byte (the
+    // last renorm byte): renorm tests, emitted bytes and the update all read
+    // x's bits in place, and the quotient reads (X >> nb) with g cleared.
+    // Per symbol: x = F, the renorm thresholds on X >> 16 (0 = not in table):
+    // one byte if > low half ((freq << 4) - 1), two if > high half ((freq << 12) - 1,
+    // 0xFFFF = never, freq >= 16); y = start << 8; z = reciprocal;
+    // w = (4096 - freq) << 8 | rsh << 24 (mad_u24 reads the low 24 bits)
     __shared__ uint4 et[256];
     __shared__ unsigned long long sh[4];
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
     {
         const uint32_t v = threadIdx.x, f = T->freq[v];
-        et[v] = make_uint4(f << TF_SHIFT, f >= TOTFREQ ? 0xFFFFFFFFu : f << (TF_SHIFT + 8), T->rcp[v],
-                           T->start[v] | (((TOTFREQ - f) & 0xFFF) << 12) | (T->rsh[v] << 24));
+        const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
+        et[v] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
+                           (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
     }
     __syncthreads();
     // Input rows k*N + 256*blk .. +255 are staged through an LDS tile of ETILE rows:
@@ -419,32 +424,39 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         return v;
     };
     uint32_t *out = reinterpret_cast<uint32_t *>(w.scratch + (size_t)b * w.region + (size_t)s * w.cap);
-    uint32_t x = RANS_L, nout = 0;  // nout = dwords stored
+    uint32_t X = RANS_L << 8, nout = 0;  // nout = dwords stored
     uint64_t acc = 0;               // pending output bits (emission order from bit 0)
     uint32_t nacc = 0;              // valid bits in acc, < 32 after every flush
     bool err = false;
     // encode_symbol (rans.rs:303-335), branchless: at most two renorm bytes
     // (x < 2^24, xmax >= 2^12); q = x / f by the exact 24-bit reciprocal.
-    // renorm bytes: x >= xmax << 8 -> 2, x >= xmax -> 1 (y >> 8 >= xmax <=> y >= xmax << 8)
-    uint32_t xmin = 0xFFFFFFFFu;  // min xmax over coded symbols: 0 = a symbol not in the table
+    // renorm bytes: x >= xmax << 8 -> 2, x >= xmax -> 1; with X = x << 8 | g,
+    // x >= f << 12 <=> (X >> 16) >= f << 4 and x >= f << 20 <=> (X >> 16) >= f << 12.
+    // Y = X >> nb = (x >> nb) << 8 | r (r < 256), so X' = Y + (start << 8) + q * (cmpl << 8)
+    // is x' << 8 | r.
+    uint32_t xmin = 0xFFFFFFFFu;  // min F over coded symbols: 0 = a symbol not in the table
+    auto renorm_bits = [&](const uint32_t F) -> uint32_t {
+        const uint32_t xh = X >> 16;
+        return xh > (F >> 16) ? 16u : (xh > (F & 0xFFFFu) ? 8u : 0u);
+    };
     auto enc_fast = [&](const uint4 e) {
         xmin = min(xmin, e.x);
-        const uint32_t nb = x >= e.y ? 16u : (x >= e.x ? 8u : 0u);
-        acc |= (uint64_t)__builtin_amdgcn_ubfe(x, 0, nb) << nacc;
+        const uint32_t nb = renorm_bits(e.x);
+        acc |= (uint64_t)__builtin_amdgcn_ubfe(X, 8, nb) << nacc;
         nacc += nb;
-        const uint32_t y = x >> nb;
-        const uint32_t q = __umulhi(y << 8, e.z) >> (e.w >> 24);          // y / f
-        x = y + (e.w & 0xFFF) + __umul24(q, (e.w >> 12) & 0xFFF);         // (y/f)*4096 + y%f + start
+        const uint32_t Y = X >> nb;
+        const uint32_t q = __umulhi(Y & ~0xFFu, e.z) >> (e.w >> 24);  // y / f
+        X = __umul24(q, e.w) + Y + e.y;                                // (y/f)*4096 + y%f + start, << 8
     };
     auto enc_step = [&](const uint4 e, bool valid) {
         err |= valid && e.x == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
-        const uint32_t nb = valid ? (x >= e.y ? 16u : (x >= e.x ? 8u : 0u)) : 0u;
-        acc |= (uint64_t)__builtin_amdgcn_ubfe(x, 0, nb) << nacc;
+        const uint32_t nb = valid ? renorm_bits(e.x) : 0u;
+        acc |= (uint64_t)__builtin_amdgcn_ubfe(X, 8, nb) << nacc;
         nacc += nb;
-        const uint32_t y = x >> nb;
-        const uint32_t q = __umulhi(y << 8, e.z) >> (e.w >> 24);
-        const uint32_t xn = y + (e.w & 0xFFF) + __umul24(q, (e.w >> 12) & 0xFFF);
-        x = valid ? xn : x;
+        const uint32_t Y = X >> nb;
+        const uint32_t q = __umulhi(Y & ~0xFFu, e.z) >> (e.w >> 24);
+        const uint32_t xn = __umul24(q, e.w) + Y + e.y;
+        X = valid ? xn : X;
     };
     uint32_t sc = 0;  // store instructions this wave issued since the last piece load
     // full dwords queue in a 4-dword shift register; every 16 bytes move to an
@@ -573,7 +585,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     if (err || xmin == 0) atomicOr(&a.status[b], 1);  // marked; converted to ZR_INVALID_INPUT by the scan
     const uint32_t bytes = nout * 4 + nacc_bytes;
     if (active) {
-        w.st_state[(size_t)b * N + s] = x;
+        w.st_state[(size_t)b * N + s] = X >> 8;
         w.st_len[(size_t)b * N + s] = bytes;
     }
     const uint64_t bs = block_sum(active ? bytes : 0, sh);
