@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B of k_enc_compact_lds shapes (ZR_CMP_VAR): parity tests and the headline bench per variant.
+# Parity tests and the headline bench once per argument, each run with ZR_CMP_VAR set to it
+# (a hook for A/B builds that read it; the committed kernels ignore it).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for V in "$@"; do
