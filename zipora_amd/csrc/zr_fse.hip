@@ -247,8 +247,14 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
     const uint8_t *in = a.in + lo;
     uint32_t *out = reinterpret_cast<uint32_t *>(a.scratch + j * a.cap);
     fv4u *out4 = reinterpret_cast<fv4u *>(out);
-    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0;
-    uint64_t nout = 0;
+    // renorm words go to a per-lane LDS ring ([slot][lane], conflict-free):
+    // every step writes its candidate word to slot nw unconditionally and
+    // advances nw only when it emits, so the step has no branch; complete
+    // 16-byte chunks leave for the scratch once per 16-symbol group.
+    __shared__ uint32_t wq[64 * 64];
+    const uint32_t lane = threadIdx.x;
+    uint32_t nw = 0;    // words emitted (ring position)
+    uint64_t nout = 0;  // words stored to the scratch (multiple of 4 until the tail)
     uint64_t x = 1;  // fse.rs:931
     bool err = false;
     auto step_e = [&](const uint4 e) {
@@ -258,24 +264,25 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
         // The word shift is branch-free (selects); only the 16-byte store of a
         // full queue branches, once per four words.
         const bool emit = x >= ((uint64_t)(f ? f : 1u) << 36);
-        q0 = emit ? q1 : q0;
-        q1 = emit ? q2 : q1;
-        q2 = emit ? q3 : q2;
-        q3 = emit ? (uint32_t)x : q3;
+        wq[((nw & 63) << 6) | lane] = (uint32_t)x;
         x = emit ? (x >> 32) : x;
-        nq += emit ? 1 : 0;
-        if (nq == 4) {
-            out4[nout >> 2] = fv4u{q0, q1, q2, q3};
-            nout += 4;
-            nq = 0;
-        }
+        nw += emit ? 1 : 0;
         const uint64_t rcp = ((uint64_t)e.y << 32) | e.x;
         const uint64_t q = mul_hi_portable(x, rcp) >> (e.w >> 16);
         x = x + (uint64_t)(e.z & 0xFFFF) + q * (uint64_t)(e.z >> 16);
     };
     auto step = [&](uint32_t sym) { step_e(s_e[sym]); };
+    auto flush = [&]() {  // complete chunks of the ring -> scratch (at most 5 per group)
+        while (nw - (uint32_t)nout >= 4) {
+            const uint32_t k = (uint32_t)nout & 63;
+            out4[nout >> 2] = fv4u{wq[(k << 6) | lane], wq[(((k + 1) & 63) << 6) | lane],
+                                   wq[(((k + 2) & 63) << 6) | lane], wq[(((k + 3) & 63) << 6) | lane]};
+            nout += 4;
+        }
+    };
     const uint64_t full = len & ~15ull;
     for (uint64_t i = len; i > full;) step(in[--i]);  // ragged top, < 16 symbols
+    flush();
     if (full && !err) {
         int64_t c = (int64_t)(full >> 4) - 1;
         if ((((uintptr_t)in) & 15) == 0) {
@@ -294,17 +301,18 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
                 for (int k = 15; k >= 0; k--) e[k] = s_e[(w[k >> 2] >> (8 * (k & 3))) & 0xFF];
 #pragma unroll
                 for (int k = 15; k >= 0; k--) step_e(e[k]);
+                flush();
                 if (err) break;
             }
         } else {
-            for (uint64_t i = full; i-- > 0;) step(in[i]);
+            for (uint64_t i = full; i-- > 0;) {
+                step(in[i]);
+                if ((i & 15) == 0) flush();
+            }
         }
     }
-    {
-        const uint32_t qs[4] = {q0, q1, q2, q3};
-        for (uint32_t i = 0; i < nq; i++) out[nout + i] = qs[4 - nq + i];
-        nout += nq;
-    }
+    flush();
+    for (; (uint32_t)nout != nw; nout++) out[nout] = wq[(((uint32_t)nout & 63) << 6) | lane];
     if (err) *a.status = ZR_INVALID_INPUT;
     a.wlen[j] = (uint32_t)(nout * 4);
     a.state[j] = x;
