@@ -263,13 +263,23 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
         // renormalize_encode: x_max = ((RANS_L >> 12) << 32) * freq = freq << 36.
         // The word shift is branch-free (selects); only the 16-byte store of a
         // full queue branches, once per four words.
-        const bool emit = x >= ((uint64_t)(f ? f : 1u) << 36);
-        wq[((nw & 63) << 6) | lane] = (uint32_t)x;
-        x = emit ? (x >> 32) : x;
+        // x < 2^48 between steps, so x >= f << 36 compares the high word only
+        const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+        const bool emit = xh >= ((f ? f : 1u) << 4);
+        wq[((nw & 63) << 6) | lane] = xl;
+        const uint32_t lo = emit ? xh : xl, hi = emit ? 0u : xh;
         nw += emit ? 1 : 0;
-        const uint64_t rcp = ((uint64_t)e.y << 32) | e.x;
-        const uint64_t q = mul_hi_portable(x, rcp) >> (e.w >> 16);
-        x = x + (uint64_t)(e.z & 0xFFFF) + q * (uint64_t)(e.z >> 16);
+        // mul_hi_portable(x, rcp) as three 32x32->64 multiply-adds: the middle
+        // sum u wraps mod 2^64 exactly like the reference's (fse.rs:618-628)
+        const uint64_t t = (uint64_t)lo * e.y + __umulhi(lo, e.x);
+        const uint64_t u = (uint64_t)hi * e.x + t;
+        const uint64_t m = (uint64_t)hi * e.y + (u >> 32);
+        const uint64_t q = m >> (e.w >> 16);
+        // x + bias + q * cmpl (wrapping); q <= x < 2^48, so q_hi * cmpl fits 24 bits
+        const uint32_t cm = e.z >> 16;
+        const uint64_t xb = (((uint64_t)hi << 32) | lo) + (e.z & 0xFFFF);
+        const uint64_t r = (uint64_t)(uint32_t)q * cm + xb;
+        x = ((uint64_t)(__umul24((uint32_t)(q >> 32), cm) + (uint32_t)(r >> 32)) << 32) | (uint32_t)r;
     };
     auto step = [&](uint32_t sym) { step_e(s_e[sym]); };
     auto flush = [&]() {  // complete chunks of the ring -> scratch (at most 5 per group)
