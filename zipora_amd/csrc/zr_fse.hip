@@ -712,7 +712,7 @@ __device__ __forceinline__ void fse_asm_load16(fv4u &dst, const fv4u *p) {
 // plus integer arithmetic.
 __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
     __shared__ uint32_t s_slot[4096];
-    __shared__ uint32_t s_ring[64 * 64];
+    __shared__ uint32_t s_ring[65 * 64];  // [slot][lane], slot 64 mirrors slot 0
     const uint32_t lane = threadIdx.x;
     const uint64_t j = (uint64_t)blockIdx.x * 64 + lane;
     const uint64_t nb = *a.nblocks;
@@ -738,6 +738,7 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
     uint32_t *ring = s_ring + lane;
     auto rd = [&](uintptr_t d) -> uint32_t { return ring[(d & 63) * 64]; };
     auto land = [&](const fv4u v, uintptr_t c) {
+        if (((4 * c) & 63) == 0) ring[64 * 64] = v.x;  // the mirror of slot 0
         ring[((4 * c + 0) & 63) * 64] = v.x;
         ring[((4 * c + 1) & 63) * 64] = v.y;
         ring[((4 * c + 2) & 63) * 64] = v.z;
@@ -751,8 +752,11 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
         // initial fill: 16 chunks (state bytes follow the words, so ctop is in bounds)
         for (int i = 0; i < 16 && fc >= cmin; i++, fc--) land(in4[fc - c0], fc);
     }
-    auto read_word = [&](uintptr_t mm) -> uint32_t {
-        return (uint32_t)((((uint64_t)rd(mm + 1) << 32) | rd(mm)) >> r8);
+    // the word at dword mm (low) and mm + 1 (high), realigned: slots mm and
+    // mm + 1 are one ds_read2st64 thanks to the mirror slot
+    auto read_word = [&](uint32_t mm) -> uint32_t {
+        const uint32_t *q = ring + (mm & 63) * 64;
+        return __builtin_amdgcn_alignbit(q[64], q[0], r8);
     };
     uint32_t nw = fast && bp >= 4 ? read_word(m) : 0u;
     auto step = [&]() -> uint32_t {
@@ -779,15 +783,15 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
     // last 1..3 bytes (one word per step at most): renormalise without that
     // branch, and with max(x, 1) folded into the word merge (after a word
     // merge x is 0 only when the decoded x and the word both are)
-    auto step_bulk = [&]() -> uint32_t {
+    // bp and m are settled once per group from the 32-bit word position m32
+    auto step_bulk = [&](uint32_t &m32) -> uint32_t {
         const uint32_t e = s_slot[x & 4095];
         const uint64_t xd = (uint64_t)(((e >> 8) & 4095) + 1) * (x >> 12) + (e >> 20);
         const bool small = xd < 65536;
         const uint64_t merged = (xd << 32) | nw | ((xd == 0 && nw == 0) ? 1u : 0u);
         x = small ? merged : xd;
-        bp -= small ? 4 : 0;
-        m -= small ? 1 : 0;
-        nw = read_word(m);
+        m32 -= small ? 1 : 0;
+        nw = read_word(m32);
         return e & 0xFF;
     };
     const uint32_t G = fast ? (uint32_t)(B.orig >> 4) : 0u;
@@ -824,8 +828,12 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
         if (g < Gl) {
             uint32_t o[4] = {0, 0, 0, 0};
             if (bp >= 68) {
+                uint32_t m32 = (uint32_t)m;
 #pragma unroll
-                for (int k = 0; k < 16; k++) o[k >> 2] |= step_bulk() << (8 * (k & 3));
+                for (int k = 0; k < 16; k++) o[k >> 2] |= step_bulk(m32) << (8 * (k & 3));
+                const uint32_t used = (uint32_t)m - m32;  // words merged by the group
+                m -= used;
+                bp -= 4ull * used;
             } else {
 #pragma unroll
                 for (int k = 0; k < 16; k++) o[k >> 2] |= step() << (8 * (k & 3));
