@@ -784,14 +784,19 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
     // branch, and with max(x, 1) folded into the word merge (after a word
     // merge x is 0 only when the decoded x and the word both are)
     // bp and m are settled once per group from the 32-bit word position m32
+    // The word is read before the slot entry (both LDS reads land by the one
+    // wait the entry needs), and max(x, 1) is a select between the word and
+    // max(word, 1) on the low dword of xd (xd < 2^16 whenever it is merged).
     auto step_bulk = [&](uint32_t &m32) -> uint32_t {
+        const uint32_t w = read_word(m32);
         const uint32_t e = s_slot[x & 4095];
+        const uint32_t w1 = max(w, 1u);
         const uint64_t xd = (uint64_t)(((e >> 8) & 4095) + 1) * (x >> 12) + (e >> 20);
         const bool small = xd < 65536;
-        const uint64_t merged = (xd << 32) | nw | ((xd == 0 && nw == 0) ? 1u : 0u);
+        const uint32_t xl = (uint32_t)xd;
+        const uint64_t merged = ((uint64_t)xl << 32) | (xl == 0 ? w1 : w);
         x = small ? merged : xd;
         m32 -= small ? 1 : 0;
-        nw = read_word(m32);
         return e & 0xFF;
     };
     const uint32_t G = fast ? (uint32_t)(B.orig >> 4) : 0u;
@@ -834,6 +839,7 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
                 const uint32_t used = (uint32_t)m - m32;  // words merged by the group
                 m -= used;
                 bp -= 4ull * used;
+                nw = read_word(m);  // the generic step's look-ahead word
             } else {
 #pragma unroll
                 for (int k = 0; k < 16; k++) o[k >> 2] |= step() << (8 * (k & 3));
