@@ -170,7 +170,10 @@ __device__ void fse_build_table(uint32_t f, FseDTab *d, unsigned long long *sh, 
     d->shift[v] = shift;
     d->bias[v] = bias;
     d->cmpl[v] = cmpl;
-    d->enc[v] = make_uint4((uint32_t)rcp, (uint32_t)(rcp >> 32), bias | (cmpl << 16), nf | (shift << 16));
+    // w: renorm threshold on the high word, (nf << 4) - 1 (x >= nf << 36 <=> x_hi > it),
+    // 0 for a symbol not in the table (encode_symbol -> None), | shift << 16
+    d->enc[v] = make_uint4((uint32_t)rcp, (uint32_t)(rcp >> 32), bias | (cmpl << 16),
+                           (nf ? (nf << 4) - 1 : 0u) | (shift << 16));
     if (v == 0) {
         d->status = ZR_OK;
         d->nsym = nsym;
@@ -253,22 +256,22 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
     // 16-byte chunks leave for the scratch once per 16-symbol group.
     __shared__ uint32_t wq[64 * 64];
     const uint32_t lane = threadIdx.x;
-    uint32_t nw = 0;    // words emitted (ring position)
+    uint32_t wa = 4 * lane;  // byte address of ring slot nw (mod 64 slots) = 4 * lane + 256 * nw
     uint64_t nout = 0;  // words stored to the scratch (multiple of 4 until the tail)
     uint64_t x = 1;  // fse.rs:931
     bool err = false;
     auto step_e = [&](const uint4 e) {
-        const uint32_t f = e.w & 0xFFFF;
-        err |= (f == 0);  // encode_symbol returns None (fse.rs:946-953)
+        const uint32_t thr = e.w & 0xFFFF;
+        err |= (thr == 0);  // encode_symbol returns None (fse.rs:946-953)
         // renormalize_encode: x_max = ((RANS_L >> 12) << 32) * freq = freq << 36.
         // The word shift is branch-free (selects); only the 16-byte store of a
         // full queue branches, once per four words.
         // x < 2^48 between steps, so x >= f << 36 compares the high word only
         const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-        const bool emit = xh >= ((f ? f : 1u) << 4);
-        wq[((nw & 63) << 6) | lane] = xl;
+        const bool emit = xh > thr;
+        *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(wq) + (wa & 0x3FFF)) = xl;
         const uint32_t lo = emit ? xh : xl, hi = emit ? 0u : xh;
-        nw += emit ? 1 : 0;
+        wa += emit ? 256u : 0u;
         // mul_hi_portable(x, rcp) as three 32x32->64 multiply-adds: the middle
         // sum u wraps mod 2^64 exactly like the reference's (fse.rs:618-628)
         const uint64_t t = (uint64_t)lo * e.y + __umulhi(lo, e.x);
@@ -283,7 +286,7 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
     };
     auto step = [&](uint32_t sym) { step_e(s_e[sym]); };
     auto flush = [&]() {  // complete chunks of the ring -> scratch (at most 5 per group)
-        while (nw - (uint32_t)nout >= 4) {
+        while ((wa >> 8) - (uint32_t)nout >= 4) {
             const uint32_t k = (uint32_t)nout & 63;
             out4[nout >> 2] = fv4u{wq[(k << 6) | lane], wq[(((k + 1) & 63) << 6) | lane],
                                    wq[(((k + 2) & 63) << 6) | lane], wq[(((k + 3) & 63) << 6) | lane]};
@@ -322,7 +325,7 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
         }
     }
     flush();
-    for (; (uint32_t)nout != nw; nout++) out[nout] = wq[(((uint32_t)nout & 63) << 6) | lane];
+    for (; (uint32_t)nout != (wa >> 8); nout++) out[nout] = wq[(((uint32_t)nout & 63) << 6) | lane];
     if (err) *a.status = ZR_INVALID_INPUT;
     a.wlen[j] = (uint32_t)(nout * 4);
     a.state[j] = x;
