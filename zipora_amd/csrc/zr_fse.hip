@@ -191,28 +191,52 @@ __global__ __launch_bounds__(256) void k_fse_tab(const uint32_t *hist, FseDTab *
     fse_build_table(hist[threadIdx.x], d, sh, norm_s, raw_s, &best);
 }
 
+// F1 histogram (fse.rs:796-851): 32 bank-spread LDS copies per workgroup (bin b,
+// copy c at b * 32 + c: lanes of a wave hit different banks even when they all
+// count the same byte, which the skewed data FSE is run on does constantly),
+// 16-byte loads, four in flight per thread, 256 KiB per workgroup.
+constexpr uint32_t FH_COPY = 32;
+constexpr uint64_t FH_CHUNK = 256 * 1024;
+__device__ __forceinline__ void fh_add4(uint32_t *h, uint32_t w, uint32_t cp) {
+    atomicAdd(&h[((w & 0xFF) << 5) + cp], 1u);
+    atomicAdd(&h[(((w >> 8) & 0xFF) << 5) + cp], 1u);
+    atomicAdd(&h[(((w >> 16) & 0xFF) << 5) + cp], 1u);
+    atomicAdd(&h[((w >> 24) << 5) + cp], 1u);
+}
 __global__ __launch_bounds__(256) void k_fse_hist(const uint8_t *in, uint64_t n, uint32_t *hist) {
-    __shared__ uint32_t h[4][257];
-    for (int i = threadIdx.x; i < 4 * 257; i += 256) (&h[0][0])[i] = 0;
+    typedef unsigned hv4u __attribute__((ext_vector_type(4)));
+    __shared__ uint32_t h[256 * FH_COPY];
+    const uint32_t tid = threadIdx.x, cp = tid & (FH_COPY - 1);
+    for (uint32_t i = tid; i < 256 * FH_COPY; i += 256) h[i] = 0;
     __syncthreads();
-    uint32_t *mine = h[threadIdx.x >> 6];
-    const uint64_t chunk = 64 * 1024;
-    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
-    for (uint64_t i = lo + threadIdx.x * 4; i < hi; i += 1024) {
-        if (i + 4 <= hi && (((uintptr_t)(in + i)) & 3) == 0) {
-            const uint32_t wv = *reinterpret_cast<const uint32_t *>(in + i);
-            atomicAdd(&mine[wv & 0xFF], 1u);
-            atomicAdd(&mine[(wv >> 8) & 0xFF], 1u);
-            atomicAdd(&mine[(wv >> 16) & 0xFF], 1u);
-            atomicAdd(&mine[wv >> 24], 1u);
-        } else {
-            for (uint64_t j = i; j < i + 4 && j < hi; j++) atomicAdd(&mine[in[j]], 1u);
-        }
+    const uint64_t lo = (uint64_t)blockIdx.x * FH_CHUNK, hi = min(n, lo + FH_CHUNK);
+    const uint64_t mis = (16 - (((uintptr_t)(in + lo)) & 15)) & 15;
+    const uint64_t blo = min(hi, lo + mis);
+    if (lo + tid < blo) atomicAdd(&h[((uint32_t)in[lo + tid] << 5) + cp], 1u);
+    const uint64_t units = (hi - blo) / 16;
+    const hv4u *q = reinterpret_cast<const hv4u *>(in + blo);
+    uint64_t u = tid;
+    for (; u + 768 < units; u += 1024) {
+        const hv4u v0 = __builtin_nontemporal_load(q + u);
+        const hv4u v1 = __builtin_nontemporal_load(q + u + 256);
+        const hv4u v2 = __builtin_nontemporal_load(q + u + 512);
+        const hv4u v3 = __builtin_nontemporal_load(q + u + 768);
+        fh_add4(h, v0.x, cp); fh_add4(h, v0.y, cp); fh_add4(h, v0.z, cp); fh_add4(h, v0.w, cp);
+        fh_add4(h, v1.x, cp); fh_add4(h, v1.y, cp); fh_add4(h, v1.z, cp); fh_add4(h, v1.w, cp);
+        fh_add4(h, v2.x, cp); fh_add4(h, v2.y, cp); fh_add4(h, v2.z, cp); fh_add4(h, v2.w, cp);
+        fh_add4(h, v3.x, cp); fh_add4(h, v3.y, cp); fh_add4(h, v3.z, cp); fh_add4(h, v3.w, cp);
     }
+    for (; u < units; u += 256) {
+        const hv4u v = q[u];
+        fh_add4(h, v.x, cp); fh_add4(h, v.y, cp); fh_add4(h, v.z, cp); fh_add4(h, v.w, cp);
+    }
+    const uint64_t tlo = blo + units * 16;
+    if (tlo + tid < hi) atomicAdd(&h[((uint32_t)in[tlo + tid] << 5) + cp], 1u);
     __syncthreads();
-    const uint32_t v = threadIdx.x;
-    const uint32_t s = h[0][v] + h[1][v] + h[2][v] + h[3][v];
-    if (s) atomicAdd(&hist[v], s);
+    // bin tid: its 32 copies, read rotated so the threads of a wave use different banks
+    uint32_t sum = 0;
+    for (uint32_t i = 0; i < FH_COPY; i++) sum += h[(tid << 5) + ((i + tid) & (FH_COPY - 1))];
+    if (sum) atomicAdd(&hist[tid], sum);
 }
 
 struct FseEncArgs {
@@ -995,7 +1019,7 @@ int32_t zr_fse_compress_dev(const zr_fse_config *c, const uint32_t *freqs_dev, c
     } else {
         ZR_HIP(hipMemsetAsync(hist, 0, 1024, s));
         timer_begin("fse_histogram", s);
-        hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, 64 * 1024)), dim3(256), 0, s, in, (uint64_t)n,
+        hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, FH_CHUNK)), dim3(256), 0, s, in, (uint64_t)n,
                            hist);
         timer_end("fse_histogram", s);
     }
@@ -1106,7 +1130,7 @@ int32_t zr_byte_histogram(const uint8_t *in, size_t n, uint32_t freqs[256]) {
     ZR_HIP(hipMalloc(&dh.p, 1024));
     ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
     ZR_HIP(hipMemset(dh.p, 0, 1024));
-    hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, 64 * 1024)), dim3(256), 0, nullptr,
+    hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, FH_CHUNK)), dim3(256), 0, nullptr,
                        (const uint8_t *)din.p, (uint64_t)n, (uint32_t *)dh.p);
     ZR_HIP(hipGetLastError());
     ZR_HIP(hipMemcpy(freqs, dh.p, 1024, hipMemcpyDeviceToHost));
