@@ -1431,9 +1431,12 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
     __shared__ uint4 et[256];
     const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
     {
+        // the k_enc_xn layout: F (renorm thresholds on X >> 16), start << 8,
+        // reciprocal, (4096 - freq) << 8 | rsh << 24
         const uint32_t v = threadIdx.x, f = T->freq[v];
-        et[v] = make_uint4(f << TF_SHIFT, f >= TOTFREQ ? 0xFFFFFFFFu : f << (TF_SHIFT + 8), T->rcp[v],
-                           T->start[v] | (((TOTFREQ - f) & 0xFFF) << 12) | (T->rsh[v] << 24));
+        const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
+        et[v] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
+                           (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
     }
     __syncthreads();
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
@@ -1443,7 +1446,7 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
     const uint8_t *in = raw + a.raw_off[b];
     uint8_t *out = enc + a.enc_off[b];
     const bool vec_out = (((uintptr_t)out) & 15) == 0;
-    uint32_t x = RANS_L;
+    uint32_t X = RANS_L << 8;  // x << 8 | a free low byte (see k_enc_xn)
     uint32_t xmin = 0xFFFFFFFFu;
     uint64_t acc = 0;
     uint32_t nacc = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0;
@@ -1452,12 +1455,13 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
     uint32_t npb = 0;  // staged 16-byte blocks
     auto enc_step = [&](const uint4 e) {  // rans.rs:303-335 (see k_enc_xn)
         xmin = min(xmin, e.x);
-        const uint32_t nb = x >= e.y ? 16u : (x >= e.x ? 8u : 0u);
-        acc |= (uint64_t)__builtin_amdgcn_ubfe(x, 0, nb) << nacc;
+        const uint32_t xh = X >> 16;
+        const uint32_t nb = xh > (e.x >> 16) ? 16u : (xh > (e.x & 0xFFFFu) ? 8u : 0u);
+        acc |= (uint64_t)__builtin_amdgcn_ubfe(X, 8, nb) << nacc;
         nacc += nb;
-        const uint32_t y = x >> nb;
-        const uint32_t q = __umulhi(y << 8, e.z) >> (e.w >> 24);
-        x = y + (e.w & 0xFFF) + __umul24(q, (e.w >> 12) & 0xFFF);
+        const uint32_t Y = X >> nb;
+        const uint32_t q = __umulhi(Y & ~0xFFu, e.z) >> (e.w >> 24);
+        X = __umul24(q, e.w) + Y + e.y;
     };
     auto push = [&]() {  // move whole dwords of acc to the queue, 16 bytes to memory
         if (nacc >= 32) {
@@ -1546,7 +1550,7 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
     }
     for (uint32_t t = 0; t < nacc / 8; t++) out[nout + t] = (uint8_t)(acc >> (8 * t));
     nout += nacc / 8;
-    for (int t = 0; t < 8; t++) out[nout + t] = (uint8_t)((uint64_t)x >> (8 * t));
+    for (int t = 0; t < 8; t++) out[nout + t] = (uint8_t)((uint64_t)(X >> 8) >> (8 * t));
     if (xmin == 0 && n) a.status[b] = ZR_INVALID_INPUT;  // "Symbol {} not in frequency table"
     a.enc_len[b] = nout + 8;
 }
