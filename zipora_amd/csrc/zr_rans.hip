@@ -1726,11 +1726,17 @@ __global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t
 // ======================================================================
 // host launchers
 // ======================================================================
+// per-stream scratch stride: a multiple of 128 B, so the encoder's 64-byte
+// bursts fill whole halves of 128-byte lines (a 16-byte multiple left every
+// stream's bursts straddling lines)
+// (A/B on one box: 0.753 -> 0.733 ms per step; 256 measured the same as 128)
+static constexpr uint64_t scratch_align() { return 128; }
+
 size_t rans_workspace_bytes(uint32_t B, uint32_t N, uint64_t max_len) {
     if (N == 0) N = 1;
     const uint64_t nblk = ceil_div(N, 256);
     const uint64_t cmax = ceil_div(max_len ? max_len : 1, N);
-    const uint64_t cap = round_up(2 * cmax + 16, 16);
+    const uint64_t cap = round_up(2 * cmax + 16, scratch_align());
     const uint64_t region = std::max<uint64_t>(round_up((uint64_t)N * cap, 256),
                                                round_up(2 * max_len + 16, 256));
     size_t t = 0;
@@ -1747,7 +1753,7 @@ int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t by
         return set_error(ZR_INVALID_INPUT, "rANS workspace too small");
     const uint64_t nblk = ceil_div(N, 256);
     const uint64_t cmax = ceil_div(max_len ? max_len : 1, N);
-    w->cap = (uint32_t)round_up(2 * cmax + 16, 16);
+    w->cap = (uint32_t)round_up(2 * cmax + 16, scratch_align());
     w->region = std::max<uint64_t>(round_up((uint64_t)N * w->cap, 256), round_up(2 * max_len + 16, 256));
     w->nblk = (uint32_t)nblk;
     uint8_t *p = reinterpret_cast<uint8_t *>(round_up((uintptr_t)ws, 256));
