@@ -1859,8 +1859,9 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         timer_begin("rans_compact", s);
         if (cmp_old)
             hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
-        else  // 16 streams per workgroup, 19 KiB window (8 workgroups per CU); block-sum scan fused in
-            hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 2>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc,
+        else  // 16 streams per workgroup, 19 KiB window (8 workgroups per CU), four 16-B loads in
+              // flight per lane (A/B: 0.140 -> 0.132 ms over two); block-sum scan fused in
+            hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 4>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc,
                                a, w);
         timer_end("rans_compact", s);
     }
