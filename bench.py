@@ -63,29 +63,70 @@ def _cpu_repeat(fn, items, threads, min_s=CPU_MIN_SECONDS):
                 return dt, passes
 
 
-def cpu_baseline(data, n, B, N, threads):
-    """The oracle (C restatement of src/entropy/rans.rs, 'port') on host cores:
-    Rans64Encoder::new + encode + decode per buffer, buffers spread over threads."""
+def host_info(threads):
+    """The GPU box's host CPU, as the CPU baseline ran on it."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"model": model, "nproc": aff, "os_cpu_count": os.cpu_count(), "threads_used": threads,
+            "note": "all-core leg = min(nproc, --cpu-threads); the GPU box allots 16 host cores per GPU"}
+
+
+def cpu_threads(args):
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return max(1, min(aff, args.cpu_threads))
+
+
+def cpu_baseline(data, n, B, N, threads, sample_bytes=None):
+    """The oracle (C restatement of src/entropy/rans.rs, 'port') on host cores, two legs:
+    (i) one thread with the reference's data structures (per-stream index vectors of
+    rans.rs:385-391 / :629-633, Vec growth; or_rans_*_mirror), (ii) every allotted core,
+    buffers spread over threads. Each: histogram + Rans64Encoder::new + encode + decode.
+    sample_bytes: code only the first sample_bytes of each buffer (bounded sample)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import concurrent.futures as cf
     import oracle_ffi as O
     O.lib()
-    nb = min(B, 4 * threads)  # bounded sample: up to 4 buffers per thread
+    m = min(n, sample_bytes) if sample_bytes else n
 
-    def one(b):
-        d = data[b * n:(b + 1) * n]
+    def one(b, mirror=False):
+        d = data[b * n:b * n + m]
         t = _table_fast(O, d)
-        enc = O.rans_encode(t, N, d)
-        dec = O.rans_decode(t, N, enc, n)
+        if mirror:
+            enc = O.rans_encode_mirror(t, N, d)
+            dec = O.rans_decode_mirror(t, N, enc, m)
+        else:
+            enc = O.rans_encode(t, N, d)
+            dec = O.rans_decode(t, N, enc, m)
         assert dec == d
         return len(enc)
 
+    nb1 = min(B, 4)
+    dt1, p1 = _cpu_repeat(lambda b: one(b, True), range(nb1), 1)
+    nb = min(B, 4 * threads)  # bounded sample: up to 4 buffers per thread
     dt, passes = _cpu_repeat(one, range(nb), threads)
-    gib = passes * nb * n / 2**30
-    return {"value": round(gib / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{passes} passes over {nb} x {n >> 20} MiB buffers (of the same uniform workload), "
-                      f"histogram+Rans64Encoder::new+encode+decode, x{N} streams, "
-                      f"{threads} threads over buffers, {dt:.2f} s wall"}
+    what = f"{m >> 20} MiB" + (f" (first {m >> 20} MiB of each {n >> 20} MiB buffer, x{N} streams over it)"
+                               if m < n else f" buffers, x{N} streams")
+    return {"value": round(passes * nb * m / 2**30 / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"all-core leg: {passes} passes over {nb} x {what} of the same uniform workload, "
+                      f"histogram+Rans64Encoder::new+encode+decode, {threads} threads over buffers, {dt:.2f} s wall",
+            "single_thread": {"value": round(p1 * nb1 * m / 2**30 / dt1, 4), "unit": "GiB/s", "cores": 1,
+                              "kind": "port",
+                              "sample": f"{p1} passes over {nb1} x {what}, reference data structures (per-stream "
+                                        f"index vectors rans.rs:385-391/:629-633, Vec growth), {dt1:.2f} s wall"},
+            "host": host_info(threads)}
 
 
 def _table_fast(O, d):
@@ -94,17 +135,20 @@ def _table_fast(O, d):
     return O.rans_table([int(x) for x in h])
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per dispatch of `kernel` from the latest committed PMC summary
-    (profiles/<round>_traffic.json, made by tools/profile_round.sh +
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def pmc_traffic(workload, kernel):
+    """HBM bytes per dispatch of `kernel` in `workload` from profiles/traffic.json, the
+    committed PMC summary of the current round (tools/profile_round.sh +
     tools/summarize_prof.py: FETCH_SIZE x2 + WRITE_SIZE, separate passes)."""
-    import glob
-    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
-    if not fs:
+    if not os.path.exists(TRAFFIC_FILE):
         return None, None
-    with open(fs[-1]) as fh:
-        t = json.load(fh).get(kernel)
-    return (t["hbm_bytes"] if t else None), os.path.relpath(fs[-1], ROOT)
+    with open(TRAFFIC_FILE) as fh:
+        doc = json.load(fh)
+    t = doc.get("workloads", {}).get(workload, {}).get(kernel)
+    src = f"profiles/traffic.json ({doc.get('source', '?')})"
+    return (round(t["hbm_bytes"]) if t else None), src
 
 
 def kernel_ms(L, name):
@@ -195,15 +239,15 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
                                f"block_size={bs >> 10} KiB ({nblk} blocks, one coder lane each)",
                    "block_size": bs, "blocks": nblk, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_fse_dec")[0],
-                     "traffic_source": pmc_traffic("k_fse_dec")[1], "kernel": "k_fse_dec",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(f"fse{bs >> 10}", "k_fse_dec")[0],
+                     "traffic_source": pmc_traffic(f"fse{bs >> 10}", "k_fse_dec")[1], "kernel": "k_fse_dec",
                      "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
         "kernels_ms": {"fse_decode": round(dec_ms, 4), "fse_encode": round(enc_ms, 4),
                        "fse_histogram": round(hist_ms, 4)},
         "compressed_bytes": clen, "ratio": round(clen / total, 5),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline_fse(host, bs, args.cpu_threads)
+        res["cpu_baseline"] = cpu_baseline_fse(host, bs, cpu_threads(args))
     return res
 
 
@@ -300,7 +344,7 @@ def run_o1(args, torch, dist, world, rank, dev, zr, L):
     ach = 2 * n / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
     extra = {"kernels_ms": {"huff_o1_encode": round(ems, 4), "huff_o1_decode": round(dms, 4)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        extra["cpu_baseline"] = cpu_baseline_o1(host, args.cpu_threads)
+        extra["cpu_baseline"] = cpu_baseline_o1(host, cpu_threads(args))
     return _line("GiB/s encode+decode (device-resident), Huffman O1, 1 GiB text over 8 GPUs", world * n * args.steps
                  / dt / 2**30, world, args, dt, "synthetic (order-1 Markov text, seed per rank)",
                  {"workload": "ContextualHuffman order-1 encode+decode, 128 MiB text per GPU (1/8 of 1 GiB)",
@@ -345,7 +389,7 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
     if world == 1 and not args.no_host_path:
         extra.update(host_pipe_rates(zr, bt, host, [1024] * R, 1, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        extra["cpu_baseline"] = cpu_baseline_blob(host, args.cpu_threads)
+        extra["cpu_baseline"] = cpu_baseline_blob(host, cpu_threads(args))
     ach = (comp + total) / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
     return _line("GiB/s encode+decode (device-resident), rANS x1 record batch, 1 M x 1 KiB", world * total *
                  args.steps / dt / 2**30, world, args, dt, "synthetic (order-1 Markov text records)",
@@ -394,6 +438,8 @@ def host_pipe_rates(zr, bt, host, lens, N, steps):
 
 def main():
     args = parse()
+    from zipora_amd import _lib as _zl
+    diag = _zl.diag_env()  # profiling ablations: garbage output, never a metric line
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -412,6 +458,8 @@ def main():
     L.zr_set_device(local)
 
     if args.workload in ("fse", "o1", "blob"):
+        if diag:
+            raise SystemExit(f"diagnostic switches set ({diag}): no metric line")
         fn = {"fse": run_fse, "o1": run_o1, "blob": run_blob}[args.workload]
         res = fn(args, torch, dist, world, rank, dev, zr, L)
         if rank == 0:
@@ -440,11 +488,10 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if not os.environ.get("ZR_ABLATE"):
+    if not diag:
         bt.raise_on_error()
-    diag = bool(os.environ.get("ZR_ABLATE"))  # diagnostic ablation builds produce garbage
-    if not diag and not torch.equal(out, raw):
-        raise SystemExit("decode mismatch after warmup")
+        if not torch.equal(out, raw):
+            raise SystemExit("decode mismatch after warmup")
 
     L.zr_timer_reset()
     L.zr_timer_enable(1)
@@ -481,6 +528,15 @@ def main():
     # dominant kernel: the fast decode (reads C compressed bytes, writes N_in bytes)
     dec_bytes = comp_bytes + total
     achieved = dec_bytes / (dec_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
+    kms = {"rans_decode": round(dec_ms, 4), "rans_encode": round(enc_ms, 4),
+           "rans_compact": round(cmp_ms, 4), "histogram": round(hist_ms, 4)}
+    if diag:  # tools/*.sh read the kernel times; no metric from a diagnostic build
+        if rank == 0:
+            print(json.dumps({"diagnostic": diag, "kernels_ms": kms, "ms_per_step": round(dt / args.steps * 1e3, 4)}),
+                  flush=True)
+        return
+    literal = B == 1
+    wl = "rans_literal" if literal else "rans"
 
     res = {
         "metric": "GiB/s encode+decode (device-resident), rANS O0, 256 MiB, 1/2/4/8 MI355X",
@@ -495,24 +551,29 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (uniform xorshift64 bytes, tests/fse_tests.rs:711-717 generator)",
-        "config": {"workload": f"rANS O0 encode+decode, {total >> 20} MiB uniform bytes per GPU as "
-                               f"{B} x {n >> 20} MiB buffers, {N}-way interleaved streams each, "
-                               f"shared table (histogram all-reduce over ranks)",
+        "config": {"workload": (f"BASELINE configs[1] as written: rANS O0 encode+decode of ONE {n >> 20} MiB "
+                                f"uniform buffer per GPU, {N}-way interleaved streams ({n // N} symbols per stream)"
+                                if literal else
+                                f"rANS O0 encode+decode, {total >> 20} MiB uniform bytes per GPU as "
+                                f"{B} x {n >> 20} MiB buffers, {N}-way interleaved streams each "
+                                f"({B * N} streams), shared table (histogram all-reduce over ranks)"),
                    "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic("k_dec_xn_fast")[0], "traffic_source": pmc_traffic("k_dec_xn_fast")[1],
+                     "traffic": pmc_traffic(wl, "k_dec_xn_fast")[0],
+                     "traffic_source": pmc_traffic(wl, "k_dec_xn_fast")[1],
                      "kernel": "k_dec_xn_fast (rans_decode)",
                      "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
-        "kernels_ms": {"rans_decode": round(dec_ms, 4), "rans_encode": round(enc_ms, 4),
-                       "rans_compact": round(cmp_ms, 4), "histogram": round(hist_ms, 4)},
+        "kernels_ms": kms,
         "compressed_bytes": comp_bytes,
         "ratio": round(comp_bytes / total, 5),
     }
     if rank == 0 and world == 1 and not args.no_host_path:
         res.update(host_pipe_rates(zr, bt, host, [n] * B, N, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(host, n, B, N, args.cpu_threads)
+        # literal config: the first 16 MiB of the buffer as its own x4096 stream set
+        res["cpu_baseline"] = cpu_baseline(host, n, B, N, cpu_threads(args),
+                                           sample_bytes=(16 << 20) if literal else None)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -13,6 +13,10 @@
  *   - no C++ exception crosses the ABI (the catch_unwind guard of c_api.rs:61-76).
  * Buffers are caller-owned. Functions without the _dev suffix take HOST memory
  * and are synchronous (they return the codec status like the Rust Result).
+ * They are thread-safe: each call leases a per-device call context (its own
+ * non-blocking HIP stream and cached device buffers), synchronises only that
+ * stream (never the device), and allocates nothing once the sizes it needs
+ * have been seen (zr_device_alloc_count).
  * Functions with the _dev suffix take DEVICE memory, are ordered on the given
  * HIP stream (hipStream_t passed as void*, NULL = default stream) and report
  * per-buffer status into a device int32 array; read it after synchronising.
@@ -61,6 +65,19 @@ int32_t zr_rans_encode(const zr_rans_table *t, uint32_t n_streams, const uint8_t
 /* Rans64Decoder::<P>::new(&enc).decode(&self, &[u8], usize)      rans.rs:449-651 */
 int32_t zr_rans_decode(const zr_rans_table *t, uint32_t n_streams, const uint8_t *in,
                        size_t in_len, uint8_t *out, size_t n);
+/* AdaptiveRans64Encoder::select_variant (rans.rs:669-681): P::N = 1, 2, 4 or 8
+ * for data sizes < 73, < 73^2, < 73^4, else */
+uint32_t zr_rans_adaptive_streams(size_t data_size);
+/* AdaptiveRans64Encoder::encode_adaptive (rans.rs:684-714): histogram of in,
+ * Rans64Encoder::<P>::new, encode with P from select_variant; *n_streams
+ * (optional) receives the P::N used, which the decoder needs */
+int32_t zr_rans_encode_adaptive(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap, size_t *out_len,
+                                uint32_t *n_streams);
+/* Exhaustive check of the encoder's reciprocal division on the device (the
+ * analogue of the reference's fast_div test, rans.rs:786-809): for every
+ * freq 1..4096 and every x < 2^24, umulhi(x << 8, rcp) >> rsh == x / freq.
+ * *mismatches receives the number of failures (0 expected). Synchronous. */
+int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches);
 
 /* ---- device-resident batch pipeline (the GPU hot path) ----
  * A batch is B independent buffers, each coded as one reference rANS stream
@@ -91,6 +108,7 @@ size_t zr_rans_dtab_bytes(void);
 /* upload host tables (Rans64Encoder::new results) as device tables */
 int32_t zr_rans_dtab_upload(const zr_rans_table *tables, uint32_t n_tables, void *dtabs_dev,
                             void *stream);
+/* Upload is stream-ordered: the host tables may be freed on return. */
 /* device histograms: per buffer (shared = 0, hist_dev has B x 256 u32) or one
  * histogram of the whole batch (shared = 1). Accumulates: zero hist_dev first
  * (zr_memset_dev). The callers this replaces count bytes on the CPU:
@@ -249,9 +267,11 @@ int32_t zr_huff_encode(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8
 /* HuffmanDecoder::decode (output_length = n)             decoder.rs:90-165 */
 int32_t zr_huff_decode(const zr_huff_tree *t, const uint8_t *in, size_t in_len, uint8_t *out,
                        size_t n);
-/* device-resident; the tree is passed by host pointer (it is uploaded with
- * the launch). Decoding synchronises the stream between its segment
- * synchronisation rounds. */
+/* device-resident; the tree is passed by host pointer (its code table or
+ * decode table is uploaded with the launch, stream-ordered). Decoding
+ * synchronises its segments on the device (bounded parallel rounds, then an
+ * exact in-order pass if needed): no host round trip; a short stream reports
+ * ZR_INVALID_INPUT ("Decoded length mismatch") in *status_dev. */
 size_t zr_huff_workspace_bytes(size_t n, size_t in_len);
 int32_t zr_huff_encode_dev(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8_t *out,
                            size_t out_cap, uint64_t *out_len_dev, int32_t *status_dev,
@@ -325,6 +345,9 @@ int32_t zr_ctx_huff_decode_dev(const zr_ctx_huff *h, int32_t nway, const uint8_t
                                size_t in_len, uint8_t *out, size_t n, void *stream);
 /* the model's order-0 tree (trees[0]) */
 int32_t zr_ctx_huff_tree0(const zr_ctx_huff *h, zr_huff_tree *t);
+
+/* number of device allocations the library has made (process lifetime) */
+int32_t zr_device_alloc_count(uint64_t *count);
 
 /* ---- device memory helpers (for hosts without a HIP binding) ---- */
 int32_t zr_malloc_dev(void **ptr, size_t bytes);

@@ -279,6 +279,129 @@ int or_rans_decode(const or_rans_table *t, uint32_t N, const uint8_t *in, size_t
     return st;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Data-structure mirror of encode_parallel / decode_parallel (rans.rs:369-420, */
+/* :555-651), for bench.py's single-thread CPU baseline only: the reference's  */
+/* per-stream Vec<usize> index vectors (8 B per input byte, :385-391 and       */
+/* :629-633), per-stream Vec<u8> outputs grown by push, and the final Vec      */
+/* built by extend. Rust's RawVec growth (doubling, minimum capacity 8 for     */
+/* u8 and 4 for usize) is followed. Same bytes as or_rans_encode/decode.       */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    size_t *p;
+    size_t n, cap;
+} ivec;
+
+static void iv_push(ivec *v, size_t x) {
+    if (v->n == v->cap) {
+        size_t c = v->cap ? 2 * v->cap : 4;
+        v->p = (size_t *)realloc(v->p, c * sizeof(size_t));
+        v->cap = c;
+    }
+    v->p[v->n++] = x;
+}
+
+static void rv_push(bvec *v, uint8_t b) { /* Vec<u8>::push: doubling from 8 */
+    if (v->n == v->cap) {
+        size_t c = v->cap ? 2 * v->cap : 8;
+        v->p = (uint8_t *)realloc(v->p, c);
+        v->cap = c;
+    }
+    v->p[v->n++] = b;
+}
+
+int or_rans_encode_mirror(const or_rans_table *t, uint32_t N, const uint8_t *in, size_t n, uint8_t *out,
+                          size_t *out_len) {
+    if (n == 0 || N <= 1 || n < N) return or_rans_encode(t, N, in, n, out, out_len);
+    uint64_t *states = (uint64_t *)malloc(sizeof(uint64_t) * N); /* vec![Rans64State::new(); N] */
+    bvec *outputs = (bvec *)calloc(N, sizeof(bvec));              /* vec![Vec::new(); N] */
+    ivec *idx = (ivec *)calloc(N, sizeof(ivec));                  /* stream_indices */
+    for (uint32_t s = 0; s < N; s++) states[s] = RANS64_L;
+    for (size_t i = 0; i < n; i++) iv_push(&idx[i % N], i); /* rans.rs:388-391 */
+    int st = OK;
+    for (uint32_t s = 0; s < N && st == OK; s++) { /* rans.rs:394-399 */
+        for (size_t k = idx[s].n; k-- > 0;) {
+            const uint8_t sym = in[idx[s].p[k]];
+            const uint32_t f = t->freq[sym];
+            if (f == 0) {
+                st = EINVAL_DATA;
+                break;
+            }
+            const uint64_t max_state = ((RANS64_L << 8) / TOTFREQ) * (uint64_t)f; /* rans.rs:319-323 */
+            while (states[s] >= max_state) {
+                rv_push(&outputs[s], (uint8_t)(states[s] & 0xFF));
+                states[s] >>= 8;
+            }
+            const uint64_t x = states[s];
+            states[s] = ((x / f) * TOTFREQ) + (x % f) + t->start[sym]; /* rans.rs:326-332 */
+        }
+    }
+    if (st == OK) {
+        bvec o = {0}; /* final_output: Vec::new() + extend_from_slice */
+        for (uint32_t s = 0; s < N; s++) bv_u64(&o, states[s]);
+        for (uint32_t s = 0; s < N; s++) bv_u32(&o, (uint32_t)outputs[s].n);
+        for (uint32_t s = 0; s < N; s++) bv_put(&o, outputs[s].p, outputs[s].n);
+        memcpy(out, o.p, o.n);
+        *out_len = o.n;
+        free(o.p);
+    }
+    for (uint32_t s = 0; s < N; s++) {
+        free(outputs[s].p);
+        free(idx[s].p);
+    }
+    free(outputs);
+    free(idx);
+    free(states);
+    return st;
+}
+
+int or_rans_decode_mirror(const or_rans_table *t, uint32_t N, const uint8_t *in, size_t len, uint8_t *out,
+                          size_t n) {
+    if (n == 0 || N <= 1 || n < N) return or_rans_decode(t, N, in, len, out, n);
+    const size_t hdr = (size_t)N * 12;
+    if (len < hdr) return EINVAL_DATA;
+    rans_dec *d = (rans_dec *)malloc(sizeof(rans_dec)); /* Rans64Decoder::new */
+    rans_dec_init(d, t);
+    uint64_t *states = (uint64_t *)malloc(sizeof(uint64_t) * N);
+    size_t *lens = (size_t *)malloc(sizeof(size_t) * N);
+    const uint8_t **data = (const uint8_t **)malloc(sizeof(uint8_t *) * N);
+    size_t *positions = (size_t *)malloc(sizeof(size_t) * N);
+    size_t total = 0, pos = 0;
+    for (uint32_t s = 0; s < N; s++, pos += 8) states[s] = rd_u64(in + pos); /* rans.rs:571-588 */
+    for (uint32_t s = 0; s < N; s++, pos += 4) {                              /* rans.rs:592-606 */
+        lens[s] = rd_u32(in + pos);
+        total += lens[s];
+    }
+    int st = OK;
+    if (pos + total > len) st = EINVAL_DATA; /* rans.rs:608-610 */
+    if (st == OK) {
+        for (uint32_t s = 0; s < N; s++) { /* rans.rs:613-617 */
+            data[s] = in + pos;
+            pos += lens[s];
+            positions[s] = lens[s]; /* rans.rs:624-626 */
+        }
+        memset(out, 0, n);             /* vec![0u8; output_length] */
+        ivec *idx = (ivec *)calloc(N, sizeof(ivec));
+        for (size_t i = 0; i < n; i++) iv_push(&idx[i % N], i); /* rans.rs:629-633 */
+        for (uint32_t s = 0; s < N && st == OK; s++) {       /* rans.rs:636-648 */
+            for (size_t k = 0; k < idx[s].n; k++) {
+                uint8_t sym;
+                st = rans_decode_symbol(d, &states[s], data[s], &positions[s], &sym);
+                if (st) break;
+                out[idx[s].p[k]] = sym;
+            }
+        }
+        for (uint32_t s = 0; s < N; s++) free(idx[s].p);
+        free(idx);
+    }
+    free(positions);
+    free(data);
+    free(lens);
+    free(states);
+    free(d);
+    return st;
+}
+
 /* ======================================================================== */
 /* FSE -- src/entropy/fse.rs                                                  */
 /* ======================================================================== */

@@ -39,6 +39,12 @@ size_t or_rans_encode_bound(size_t n, uint32_t n_streams);
 int or_rans_encode(const or_rans_table *t, uint32_t n_streams, const uint8_t *in, size_t n,
                    uint8_t *out, size_t *out_len);
 /* Rans64Decoder::decode (rans.rs:510-651). */
+/* The same two calls with the reference's data structures (per-stream index
+ * vectors, Vec growth) -- bench.py's single-thread CPU baseline. */
+int or_rans_encode_mirror(const or_rans_table *t, uint32_t n_streams, const uint8_t *in, size_t n,
+                          uint8_t *out, size_t *out_len);
+int or_rans_decode_mirror(const or_rans_table *t, uint32_t n_streams, const uint8_t *in, size_t in_len,
+                          uint8_t *out, size_t n);
 int or_rans_decode(const or_rans_table *t, uint32_t n_streams, const uint8_t *in, size_t in_len,
                    uint8_t *out, size_t n);
 

@@ -54,6 +54,8 @@ def lib():
         L.or_rans_encode.argtypes = [ctypes.POINTER(RansTable), ctypes.c_uint32, u8p, sz, u8p,
                                      ctypes.POINTER(sz)]
         L.or_rans_decode.argtypes = [ctypes.POINTER(RansTable), ctypes.c_uint32, u8p, sz, u8p, sz]
+        L.or_rans_encode_mirror.argtypes = L.or_rans_encode.argtypes
+        L.or_rans_decode_mirror.argtypes = L.or_rans_decode.argtypes
         L.or_fse_config_default.argtypes = [ctypes.POINTER(FseConfig)]
         L.or_fse_compress_bound.argtypes = [sz, ctypes.POINTER(FseConfig)]
         L.or_fse_compress_bound.restype = sz
@@ -139,6 +141,23 @@ def rans_decode(table, n_streams, enc, n):
     b, ln = _buf(enc)
     out = _out(n)
     _check(lib().or_rans_decode(ctypes.byref(table), n_streams, b, ln, out, n), "rans_decode")
+    return ctypes.string_at(out, n)
+
+
+def rans_encode_mirror(table, n_streams, data):
+    """rans_encode with the reference's data structures (index vectors, Vec growth)."""
+    b, n = _buf(data)
+    out = _out(lib().or_rans_encode_bound(n, n_streams))
+    ol = sz(0)
+    _check(lib().or_rans_encode_mirror(ctypes.byref(table), n_streams, b, n, out, ctypes.byref(ol)),
+           "rans_encode_mirror")
+    return ctypes.string_at(out, ol.value)
+
+
+def rans_decode_mirror(table, n_streams, enc, n):
+    b, ln = _buf(enc)
+    out = _out(n)
+    _check(lib().or_rans_decode_mirror(ctypes.byref(table), n_streams, b, ln, out, n), "rans_decode_mirror")
     return ctypes.string_at(out, n)
 
 

@@ -94,3 +94,39 @@ def test_synth_is_deterministic(zr, oracle):
     assert hist[0] > hist[1] > hist[10] > hist[100]
     t = zr.synth("t", 1 << 16)
     assert len(set(t)) <= 64
+
+
+def test_adaptive_select_variant_thresholds(zr):
+    """AdaptiveRans64Encoder::select_variant (rans.rs:669-681) and the reference's
+    test (rans.rs:864-878); host code, no GPU."""
+    a = zr.AdaptiveRans64Encoder()
+    assert [a.select_variant(n) for n in (50, 100, 10000, 30000000)] == ["x1", "x2", "x4", "x8"]
+    edges = {0: "x1", 72: "x1", 73: "x2", 73 ** 2 - 1: "x2", 73 ** 2: "x4", 73 ** 4 - 1: "x4", 73 ** 4: "x8"}
+    assert {n: a.select_variant(n) for n in edges} == edges
+
+
+def test_stream_count_limit_checked_before_any_launch(zr):
+    """the 2^27-stream limit is refused up front (no kernel, no timer)."""
+    from zipora_amd import _lib
+    lib = zr.load()
+    bt = _lib.RansBatch()
+    bt.n_buffers, bt.n_streams, bt.max_len = 1, 1 << 27, 1 << 28
+    for fn in (lib.zr_rans_encode_batch_dev, lib.zr_rans_decode_batch_dev):
+        assert fn(ctypes.byref(bt), None, None, None, 0, None) == _lib.ZR_UNSUPPORTED
+        assert "2^27" in zr.last_error()
+
+
+def test_diagnostic_switches_are_tools_only():
+    """the product library reads no diagnostic environment
+    switches (they exist only in the -DZR_DIAG tools build) and bench.py refuses
+    to print a metric line while one is set."""
+    import subprocess
+    import sys
+    src = open(os.path.join(ROOT, "zipora_amd", "csrc", "zr_rans.hip")).read()
+    for m in re.finditer(r'getenv\("(ZR_[A-Z_]+)"\)', src):
+        head = src[:m.start()]
+        assert head.count("#ifdef ZR_DIAG") > head.count("#endif") - head.count("#ifndef"), m.group(1)
+    env = dict(os.environ, ZR_ABLATE="1")
+    r = subprocess.run([sys.executable, "-c", "import zipora_amd._lib as l; print(l.diag_env())"],
+                       cwd=ROOT, env=env, capture_output=True, text=True)
+    assert "ZR_ABLATE" in r.stdout

@@ -1,0 +1,235 @@
+"""Known-answer vectors C1-C6, derived by stepping the reference source by hand
+(round 2; SURVEY.md Appendix B holds B1-B14). Each vector's derivation is in
+the comment above it: the table the reference builds, then the coder state
+after every step that matters. They pin the CPU oracle (not gpu) and the HIP
+path through the C ABI (gpu) to bytes that neither of them produced.
+
+Arithmetic is the reference's, in release mode (wrapping u64, Cargo.toml
+[profile.release]). rANS: L = 2^16, M = 4096, encode_symbol renormalises while
+x >= 4096 * f (rans.rs:319-323), then x = (x / f) * 4096 + x % f + start
+(rans.rs:326-332). FSE: state starts at 1 (fse.rs:931), renormalize_encode
+emits the low u32 once if x >= f << 36 (fse.rs:680-700), encode_symbol is
+x + bias + (mul_hi(x, rcp) >> shift) * (4096 - f) (fse.rs:632-648).
+"""
+import pytest
+
+# ---------------------------------------------------------------------------
+# Shared rANS table for C1/C2: raw freqs {a: 1, b: 1000, c: 1000}.
+# normalize_frequencies (rans.rs:238-299): total = 2001, 3 symbols -> 1 each,
+# remaining = initial_remaining = 4093. Pass 2: a += 1*4093/2001 = 2 (-> 3),
+# b += 1000*4093/2001 = 2045 (-> 2046), c += 2045 (-> 2046), remaining = 1.
+# Pass 3: the largest raw freq whose norm is < 1024 is a (b, c are 2046), so
+# a -> 4. Table: a = 4 @ 0, b = 2046 @ 4, c = 2046 @ 2050.
+RAW_ABC = {0x61: 1, 0x62: 1000, 0x63: 1000}
+
+# C1 -- rANS x1, a two-byte renormalisation (f = 4 < 16). encode(b"abbbbbb")
+# codes the string backwards from x = 65536:
+#   b: 65536 / 2046 = 32 r 64        -> 32*4096 + 64 + 4    = 131140
+#   b: 131140 = 64*2046 + 196        -> 262144 + 196 + 4    = 262344
+#   b: 262344 = 128*2046 + 456       -> 524288 + 460        = 524748
+#   b: 524748 = 256*2046 + 972       -> 1048576 + 976       = 1049552
+#   b: 1049552 = 512*2046 + 2000     -> 2097152 + 2004      = 2099156
+#   b: 2099156 = 1025*2046 + 2006    -> 4198400 + 2010      = 4200410 = 0x4017DA
+#   a: 4200410 >= 4096*4: emit 0xDA, x = 0x4017 = 16407 >= 16384: emit 0x17,
+#      x = 0x40 = 64 -> (64/4)*4096 + 0 + 0 = 65536
+# output = renorm bytes in emission order | state u64 LE (rans.rs:354-366).
+C1 = ("abbbbbb", "da17" + "0000010000000000")
+
+# C2 -- rANS x4 (rans.rs:369-420), every stream non-empty. encode(b"abcabcabcabc"):
+# stream s holds symbols s, s+4, s+8, coded backwards from 65536.
+#   s0 = (a, b, c): c -> 32*4096 + 64 + 2050 = 133186; b -> 133186 = 65*2046 + 196
+#       -> 266240 + 200 = 266440 = 0x410C8; a: emit 0xC8, x = 0x410 = 1040
+#       -> 260*4096 = 1064960 = 0x104000
+#   s1 = (b, c, a): a: 65536 >= 16384 emit 0x00, x = 256 -> 64*4096 = 262144;
+#       c -> 262144 = 128*2046 + 256 -> 524288 + 256 + 2050 = 526594;
+#       b -> 526594 = 257*2046 + 772 -> 1052672 + 776 = 1053448 = 0x101308
+#   s2 = (c, a, b): b -> 131140 = 0x20044; a: emit 0x44, x = 0x200 -> 524288;
+#       c -> 524288 = 256*2046 + 512 -> 1048576 + 2562 = 1051138 = 0x100A02
+#   s3 = s0's symbols: 1064960, stream byte 0xC8
+# output = 4 states u64 | 4 lengths u32 (all 1) | streams c8 00 44 c8
+C2 = ("abcabcabcabc",
+      "0040100000000000" "0813100000000000" "020a100000000000" "0040100000000000"
+      "01000000" "01000000" "01000000" "01000000" "c80044c8")
+
+# C3 -- FSE 0xF5, two symbols, two 32-bit words. fse_compress(b"ab" * 50):
+# normalize_frequencies_exact (fse.rs:513-580): a = b = 50*4096/100 = 2048.
+# init_enc_symbol (fse.rs:583-615), f = 2048: shift = 11, rcp = 2^63,
+# rcp_shift = 10, so q = mul_hi(x, 2^63) >> 10 = x >> 11 and
+# x' = x + start + (x >> 11) * 2048: one bit per symbol (a adds 0, b adds 2048
+# to the low part). From x = 1, coding b, a, b, a, ... (backwards) the state
+# doubles per symbol; it reaches f << 36 = 2^47 twice and emits its low u32
+# each time: 0xAAAAA801 then 0xAAAAAAAA (alternating bits of a/b), and ends
+# at 0x00005555555552AA.
+# output = F5 | len 100 | log 12 | nsym 2 | (61, 2048) (62, 2048) | words | state
+C3 = ("ab" * 50,
+      "f5" "64000000" "0c" "0200" "6100080000" "6200080000" "01a8aaaa" "aaaaaaaa" "aa52555555550000")
+
+# C4 -- FSE 0xF6 (fse.rs:970-1044). parallel_blocks = Some(2), block_size = 100.
+# compress takes the parallel path only when len > 2 * block_size (fse.rs:869-871),
+# so the shortest 0xF6 stream has three blocks; here 250 bytes -> 100, 100, 50.
+# Data: byte i = b"abc"[(7 i) mod 3] = b"abc"[i mod 3]: 84 a, 83 b, 83 c. The
+# global table (fse.rs:513-580 on the histogram of all 250 bytes):
+# a = 84*4096/250 = 1376, b = c = 83*4096/250 = 1359 -> 4094 assigned, the
+# deficit of 2 goes to the largest raw count: a = 1378 = 0x562, b = c = 0x54F.
+# It is written into every coded block; the 50-byte block is below 100 and is
+# stored raw (len | FF | bytes, fse.rs:892-904).
+# Each coded block: len 100 | 0C | nsym 3 | (61, 0x562) (62, 0x54F) (63, 0x54F)
+# | words | state (the block bodies are 0x2E, 0x2E and 0x37 bytes).
+C4_DATA = bytes(b"abc"[(7 * i) % 3] for i in range(250))
+C4 = ("f6" "03000000" "2e000000" "2e000000" "37000000"
+      "64000000" "0c" "0300" "6162050000" "624f050000" "634f050000"
+      "4173b44a45c9becfebde840282a0af7e" "65c3c7b574000000"
+      "64000000" "0c" "0300" "6162050000" "624f050000" "634f050000"
+      "903bc3bfec212c83582aaf5b2e061ca4" "7ad84505cb000000"
+      "32000000" "ff" + C4_DATA[200:].hex())
+
+# C5 -- FSE freq == 1 with the wrapping mul_hi (fse.rs:618-628). A static table
+# (zr_fse_compress_freqs / FseEncoder with adaptive = false) of raw = normalised
+# freqs {00: 2, 41 'A': 1, 42: 3000, 43: 1093} (sum 4096, normalize_exact is the
+# identity). For f = 1, rcp = ~0, shift 0, bias = start + 4095, and for a state
+# x = a_hi * 2^32 + a_lo the middle sum b_lo*a_hi + b_hi*a_lo + (x0 >> 32) =
+# (2^32 - 1)(a_hi + a_lo) + ... wraps mod 2^64 once a_hi + a_lo > 2^32: then
+# q = x - 1 - 2^32 instead of x - 1.
+# Construction: x* = 0x3_FFFF_FFFE (a_hi = 3, a_lo = 2^32 - 2: wraps). Decoding
+# backwards from x* with the table (slot = x & 4095, x' = f*(x >> 12) + slot - start)
+# visits 84 symbols and lands on x = 1, the encoder's initial state; symbol 00
+# (start 0, f = 2) keeps x = 1 fixed in both directions. So the input
+#   A | those 84 symbols | 00 * 115          (200 bytes)
+# drives the encoder (which codes it backwards, no renormalisation below
+# 2^36) to x* just before it codes 'A'. Coding 'A' (start 2):
+#   true:    x*4096 + 2           = 0x3FFFFFFFE002
+#   wrapped: minus 4095 * 2^32    = 0x3000FFFFE002   (the reference's state)
+# output = F5 | len 200 | 0C | nsym 4 | table | no words | state 0x3000FFFFE002.
+# The stream does NOT decode back to the input (the reference's own bug);
+# decoders must agree with each other on what it does decode to.
+C5_FREQS = {0x00: 2, 0x41: 1, 0x42: 3000, 0x43: 1093}
+C5_STATE = 0x3_FFFF_FFFE
+
+
+def c5_input():
+    """'A' + the symbols decoded from x* down to state 1 + padding (see C5)."""
+    start, c = {}, 0
+    for s in sorted(C5_FREQS):
+        start[s] = c
+        c += C5_FREQS[s]
+    alias = []
+    for s in sorted(C5_FREQS):
+        alias += [s] * C5_FREQS[s]
+    x, chain = C5_STATE, []
+    while x != 1:
+        s = alias[x & 4095]
+        chain.append(s)
+        x = C5_FREQS[s] * (x >> 12) + (x & 4095) - start[s]
+        assert len(chain) < 200
+    return bytes([0x41] + chain + [0x00] * (200 - 1 - len(chain)))
+
+
+C5 = ("f5" "c8000000" "0c" "0400" "0002000000" "4101000000" "42b80b0000" "4345040000"
+      "02e0ffff00300000")
+
+
+def _c5_freqs():
+    f = [0] * 256
+    for s, v in C5_FREQS.items():
+        f[s] = v
+    return f
+
+
+# C6 -- Huffman chain code longer than 32 bits (tree.rs:52-133, encoder.rs:88-131).
+# Frequencies: symbol 0x40 + i has frequency i for i = 1..36. BinaryHeap<Reverse>
+# pops the HIGHEST frequency first (SURVEY finding 0.6) and there are no ties
+# (every merged node outweighs every leaf): N1 = (0x64, 0x63), N2 = (N1, 0x62), ...
+# root = (N34, 0x41). Left = 0, right = 1 (tree.rs:187-208): 0x41 = "1",
+# 0x42 = "01", ..., 0x62 = 0^33 1, 0x63 = 0^34 1 (35 bits), 0x64 = 0^35 (35 bits).
+# encode([0x64, 0x41, 0x63]): 35 zeros, 1, 34 zeros, 1 = 71 bits; LSB-first
+# packing puts bit 35 in byte 4 (0x08) and bit 70 in byte 8 (0x40).
+C6_FREQS = {0x40 + i: i for i in range(1, 37)}
+C6 = (bytes([0x64, 0x41, 0x63]), "000000000800000040")
+
+
+def _c6_freqs():
+    f = [0] * 256
+    for s, v in C6_FREQS.items():
+        f[s] = v
+    return f
+
+
+def _raw_abc():
+    f = [0] * 256
+    for s, v in RAW_ABC.items():
+        f[s] = v
+    return f
+
+
+# ------------------------------------------------------------- CPU: the oracle
+def test_c1_c2_oracle(oracle):
+    t = oracle.rans_table(_raw_abc())
+    assert (t.freq[0x61], t.start[0x61], t.freq[0x62], t.start[0x62], t.freq[0x63], t.start[0x63]) == \
+        (4, 0, 2046, 4, 2046, 2050)
+    assert oracle.rans_encode(t, 1, C1[0].encode()).hex() == C1[1]
+    assert oracle.rans_decode(t, 1, bytes.fromhex(C1[1]), 7) == C1[0].encode()
+    assert oracle.rans_encode(t, 4, C2[0].encode()).hex() == C2[1]
+    assert oracle.rans_decode(t, 4, bytes.fromhex(C2[1]), 12) == C2[0].encode()
+
+
+def test_c3_c4_oracle(oracle):
+    assert oracle.fse_compress(C3[0].encode()).hex() == C3[1]
+    assert oracle.fse_decompress(bytes.fromhex(C3[1])) == C3[0].encode()
+    cfg = oracle.fse_config(parallel_blocks=2, block_size=100)
+    assert oracle.fse_compress(C4_DATA, cfg).hex() == C4
+    assert oracle.fse_decompress(bytes.fromhex(C4)) == C4_DATA
+
+
+def test_c5_oracle_wraps(oracle):
+    d = c5_input()
+    assert len(d) == 200 and d[0] == 0x41
+    # the state before 'A' is coded really is one the portable mul_hi gets wrong
+    assert oracle.lib().or_fse_mul_hi(C5_STATE, (1 << 64) - 1) != C5_STATE - 1
+    assert oracle.fse_compress_freqs(d, _c5_freqs()).hex() == C5
+    assert oracle.fse_decompress(bytes.fromhex(C5)) != d  # the reference's round trip fails here
+
+
+def test_c6_oracle(oracle):
+    t = oracle.huff_tree(_c6_freqs())
+    codes = oracle.huff_codes(t)
+    assert codes[0x64] == "0" * 35 and codes[0x63] == "0" * 34 + "1" and codes[0x41] == "1"
+    assert oracle.huff_encode(t, C6[0]).hex() == C6[1]
+    assert oracle.huff_decode(t, bytes.fromhex(C6[1]), 3) == C6[0]
+
+
+# ------------------------------------------------------- GPU: the HIP C ABI
+@pytest.mark.gpu
+def test_c1_c2_gpu(zr):
+    enc1 = zr.Rans64Encoder(_raw_abc(), 1)
+    assert enc1.encode(C1[0].encode()).hex() == C1[1]
+    assert zr.Rans64Decoder(enc1).decode(bytes.fromhex(C1[1]), 7) == C1[0].encode()
+    enc4 = zr.Rans64Encoder(_raw_abc(), 4)
+    assert enc4.encode(C2[0].encode()).hex() == C2[1]
+    assert zr.Rans64Decoder(enc4).decode(bytes.fromhex(C2[1]), 12) == C2[0].encode()
+
+
+@pytest.mark.gpu
+def test_c3_c4_gpu(zr):
+    assert zr.fse_compress(C3[0].encode()).hex() == C3[1]
+    assert zr.fse_decompress(bytes.fromhex(C3[1])) == C3[0].encode()
+    cfg = zr.FseConfig(parallel_blocks=2, block_size=100)
+    assert zr.fse_compress_with_config(C4_DATA, cfg).hex() == C4
+    assert zr.fse_decompress(bytes.fromhex(C4)) == C4_DATA
+
+
+@pytest.mark.gpu
+def test_c5_gpu_wrapping_mul_hi(zr, oracle):
+    """k_fse_enc's restated portable mul_hi on a state where it wraps."""
+    d = c5_input()
+    enc = zr.FseEncoder(zr.FseConfig(adaptive=False))
+    enc._freqs = _c5_freqs()  # the static table (FseEncoder.table kept when adaptive = false)
+    got = enc.compress(d)
+    assert got.hex() == C5
+    assert zr.fse_decompress(got) == oracle.fse_decompress(got)
+
+
+@pytest.mark.gpu
+def test_c6_gpu(zr):
+    e = zr.HuffmanEncoder.from_frequencies(_c6_freqs())
+    assert e.encode(C6[0]).hex() == C6[1]
+    assert zr.HuffmanDecoder(e.tree()).decode(bytes.fromhex(C6[1]), 3) == C6[0]

@@ -1,0 +1,320 @@
+"""Round-2 rANS parity on the MI355X through the C ABI, against the oracle:
+the literal BASELINE configs[1] at full size, both launch shapes of the coders,
+wrapped-sum tables built on the device, the encoder's reciprocal division
+checked exhaustively, allocation-free host calls from two threads, the
+adaptive encoder, the pipe's error drain, the Huffman decoder's in-order
+fallback, and the bench's N > 1 table exchange."""
+import os
+import random
+import socket
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _fill(bt, datas):
+    import torch
+    raw = bt.new_raw()
+    for b, d in enumerate(datas):
+        o = bt.raw_off_host[b]
+        if d:
+            raw[o:o + len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+    return raw
+
+
+def test_rans_literal_config_full_size(zr, oracle):
+    """BASELINE configs[1] as written: ONE 256 MiB uniform buffer, 4096-way
+    interleaved streams (rans.rs:369-420), 65,536 symbols per stream. Encoded on
+    the device (histogram -> Rans64Encoder::new -> encode), byte-compared with the
+    oracle's Rans64Encoder::encode, decoded back."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    n, N = 256 << 20, 4096
+    data = zr.synth("u", n, seed=0x9E3779B97F4A7C15)
+    bt = RansDeviceBatch([n], N, shared_table=True)
+    raw = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    t = oracle.rans_table(oracle.histogram(data))
+    ref = oracle.rans_encode(t, N, data)
+    got = bt.encoded(enc, 0)
+    assert len(got) == len(ref)
+    assert got == ref
+    del ref, got
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    assert torch.equal(out[:n], raw)
+
+
+@pytest.mark.parametrize("N,B", [(4096, 24), (1000, 70)])
+def test_rans_wide_shape_ragged(zr, oracle, N, B):
+    """More than 2^16 streams in the batch: 256-lane encoder and 1024-lane decoder
+    workgroups, with ragged, tiny (x1 layout) and empty buffers mixed in."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    rnd = random.Random(N)
+    base = [0, 1, N - 1, N, N + 1, 50000, 123457, 1 << 18, 3 * N + 7]
+    lens = [base[i % len(base)] if i < len(base) else rnd.randrange(N, 40 * N) for i in range(B)]
+    assert B * N > (1 << 16)
+    datas = [zr.synth("u" if b % 3 else "z", n, seed=77 + b) for b, n in enumerate(lens)]
+    bt = RansDeviceBatch(lens, N)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    for b, d in enumerate(datas):
+        t = oracle.rans_table(oracle.histogram(d))
+        assert bt.encoded(enc, b) == oracle.rans_encode(t, N, d), f"buffer {b} (n={len(d)})"
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    for b, d in enumerate(datas):
+        assert bt.raw_of(out, b) == d
+
+
+@pytest.mark.parametrize("N", [64, 100, 1000, 4095, 4097])
+def test_rans_narrow_shape_ragged(zr, oracle, N):
+    """Few streams (one-wave workgroups): stream counts that are not multiples of
+    the 64-lane workgroup, long streams, a shared table."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    lens = [300000 + 13 * N, 5 * N + 3, N]
+    datas = [zr.synth("t", n, seed=5 + b) for b, n in enumerate(lens)]
+    bt = RansDeviceBatch(lens, N, shared_table=True)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    t = oracle.rans_table(oracle.histogram(b"".join(datas)))
+    for b, d in enumerate(datas):
+        assert bt.encoded(enc, b) == oracle.rans_encode(t, N, d), f"buffer {b}"
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    for b, d in enumerate(datas):
+        assert bt.raw_of(out, b) == d
+
+
+def _dtab_words(bt, k=0):
+    w = bt.tables.cpu().numpy().view(np.uint32)
+    per = bt.tables.numel() // 4 // bt.n_tables
+    return w[k * per:(k + 1) * per]
+
+
+def test_device_table_wrapped_total(zr, oracle):
+    """k_tab on histograms whose u32 sum wraps (rans.rs:209): the min(remaining)
+    clamp of rans.rs:264-271 binds. Device table == oracle == host table."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    rnd = random.Random(11)
+    hists = []
+    h = [0] * 256
+    h[97], h[98], h[99] = 0xFFFFFFF0, 20, 5  # total wraps to 9
+    hists.append(h)
+    h = [0] * 256
+    h[0], h[255] = 0x80000000, 0x80000001  # total wraps to 1
+    hists.append(h)
+    for _ in range(30):
+        h = [rnd.choice([0, 0, 1, rnd.randrange(1, 1000)]) for _ in range(256)]
+        for _ in range(rnd.randrange(1, 4)):
+            h[rnd.randrange(256)] = rnd.randrange(1 << 30, 1 << 32)
+        if sum(h) & 0xFFFFFFFF == 0:
+            h[3] += 1
+        hists.append(h)
+    assert all(sum(h) >= (1 << 32) for h in hists)
+    bt = RansDeviceBatch([1] * len(hists), 1, shared_table=False)
+    bt.hist.copy_(torch.tensor(np.array(hists, dtype=np.uint32).view(np.int32).reshape(-1)).cuda())
+    bt.tables_from_hist()
+    torch.cuda.synchronize()
+    for k, h in enumerate(hists):
+        t = oracle.rans_table(h)
+        w = _dtab_words(bt, k)
+        freq, start, slot = w[4:260], w[260:516], w[1028:1028 + 4096]
+        assert list(freq) == list(t.freq), f"hist {k}"
+        assert list(start) == list(t.start), f"hist {k}"
+        host = zr.Rans64Encoder(h, 1).table
+        assert list(host.freq) == list(t.freq)
+        owner = np.zeros(4096, dtype=np.int64)
+        for s in range(256):
+            owner[t.start[s]:t.start[s] + t.freq[s]] = s
+        assert (slot & 0xFF).tolist() == owner.tolist(), f"hist {k}"
+
+
+def test_encoder_reciprocal_exhaustive(zr):
+    """umulhi(x << 8, rcp) >> rsh == x / f for every f in 1..4096, x < 2^24 (the
+    analogue of the reference's fast_div test, rans.rs:786-809), on the device."""
+    assert zr.selftest_reciprocal() == 0
+
+
+def test_host_calls_allocation_free_two_threads(zr, oracle):
+    """10k x 1 KiB records through the synchronous zr_rans_encode/decode from two
+    host threads: after warm-up the library allocates nothing (zr_device_alloc_count)."""
+    recs = [zr.synth("t", 1024, seed=100 + i) for i in range(10000)]
+    freqs = oracle.histogram(b"".join(recs))
+    enc = zr.Rans64Encoder(freqs, 1)
+    dec = zr.Rans64Decoder(enc)
+    out = [None] * len(recs)
+    errors = []
+
+    def run(idx, barrier):
+        try:
+            barrier.wait()
+            for i in idx:
+                e = enc.encode(recs[i])
+                out[i] = e
+                assert dec.decode(e, 1024) == recs[i]
+        except Exception as ex:  # noqa: BLE001
+            errors.append(ex)
+
+    def two_threads(lo, hi):
+        b = threading.Barrier(2)
+        ts = [threading.Thread(target=run, args=(range(lo + k, hi, 2), b)) for k in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors[:2]
+
+    two_threads(0, 400)  # warm-up: both threads' call contexts grow to 1 KiB records
+    before = zr.device_alloc_count()
+    two_threads(400, len(recs))
+    after = zr.device_alloc_count()
+    assert after == before, f"{after - before} device allocations after warm-up"
+    t = oracle.rans_table(freqs)
+    for i in range(0, len(recs), 97):
+        assert out[i] == oracle.rans_encode(t, 1, recs[i])
+
+
+def test_adaptive_encoder(zr, oracle):
+    """AdaptiveRans64Encoder (rans.rs:655-721) incl. the reference's own test
+    (rans.rs:864-878): thresholds 73, 73^2, 73^4 and encode_adaptive."""
+    a = zr.AdaptiveRans64Encoder()
+    assert a.select_variant(50) == "x1"
+    assert a.select_variant(100) == "x2"
+    assert a.select_variant(10000) == "x4"
+    assert a.select_variant(30000000) == "x8"
+    for data in (b"test data for adaptive encoding", zr.synth("t", 73), zr.synth("z", 6000),
+                 zr.synth("u", 100000), b""):
+        N = {"x1": 1, "x2": 2, "x4": 4, "x8": 8}[a.select_variant(len(data))]
+        got = a.encode_adaptive(data)
+        assert got
+        t = oracle.rans_table(oracle.histogram(data))
+        assert got == oracle.rans_encode(t, N, data)
+
+
+def test_pipe_error_then_reuse(zr, oracle):
+    """an error return of the host pipe drains its streams and
+    frees its slots, so the same pipe then codes a smaller batch correctly."""
+    import torch
+    from zipora_amd.device import RansHostPipe
+    datas = [zr.synth("t", 1024, seed=i) for i in range(50)]
+    freqs = oracle.histogram(b"".join(datas))
+    pipe = RansHostPipe(zr.Rans64Encoder(freqs, 1).table, 1, 16 << 10)
+    lens = [1024] * 50
+    raw_off, _, rb, _ = pipe.layout(lens)
+    raw = torch.zeros(rb, dtype=torch.uint8, pin_memory=True)
+    for b, d in enumerate(datas):
+        raw[int(raw_off[b]):int(raw_off[b]) + 1024] = torch.frombuffer(bytearray(d), dtype=torch.uint8)
+    small = torch.zeros(3000, dtype=torch.uint8, pin_memory=True)  # far below 50 encoded records
+    with pytest.raises(zr.ZiporaError):
+        pipe.encode_packed(lens, raw, raw_off, small)
+    lens2 = [1024] * 3
+    raw_off2, _, rb2, eb2 = pipe.layout(lens2)
+    raw2 = raw[:rb2].clone().pin_memory()
+    enc2 = torch.zeros(eb2, dtype=torch.uint8, pin_memory=True)
+    enc_off, enc_len, st, total = pipe.encode_packed(lens2, raw2, raw_off2, enc2)
+    assert (st == 0).all()
+    t = oracle.rans_table(freqs)
+    e = enc2.numpy()
+    for b in range(3):
+        o = int(enc_off[b])
+        assert e[o:o + int(enc_len[b])].tobytes() == oracle.rans_encode(t, 1, datas[b])
+    pipe.close()
+
+
+def test_huffman_decode_inorder_fallback(zr, oracle):
+    """A stream whose guessed segment starts never resynchronise by themselves
+    (a 3-bit all-zero code repeated over 70+ segments): the decoder's device
+    rounds run out and its in-order pass finishes the job, without a host round
+    trip. Output == oracle (decoder.rs:90-165)."""
+    data = b"a" * 100000 + b"bcd"
+    e = zr.HuffmanEncoder(data)
+    bits = e.encode(data)
+    t = oracle.huff_tree(oracle.histogram(data))
+    assert bits == oracle.huff_encode(t, data)
+    assert max(len(c) for c in oracle.huff_codes(t).values()) == 3
+    assert zr.HuffmanDecoder(e.tree()).decode(bits, len(data)) == data
+    with pytest.raises(zr.ZiporaError):  # "Decoded length mismatch"
+        zr.HuffmanDecoder(e.tree()).decode(bits[:1000], 2700)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        import zipora_amd as zr
+        from zipora_amd import dist as zd
+        from zipora_amd.device import RansDeviceBatch
+        import oracle_ffi as O
+        lens = [200000 + 31 * rank, 70000]
+        datas = [zr.synth("z", n, seed=zd.shard_seed(9, rank) + b) for b, n in enumerate(lens)]
+        bt = RansDeviceBatch(lens, 4096, shared_table=True)
+        raw = _fill(bt, datas)
+        enc = bt.new_enc()
+        # bench.py's N > 1 step: device histogram -> all-reduce -> k_tab -> encode
+        bt.histogram(raw)
+        zd.allreduce_histogram(bt.hist)
+        bt.tables_from_hist()
+        bt.encode(raw, enc)
+        torch.cuda.synchronize()
+        bt.raise_on_error()
+        shards = [None] * world
+        dist.all_gather_object(shards, b"".join(datas))
+        t = O.rans_table(O.histogram(b"".join(shards)))
+        ok = all(bt.encoded(enc, b) == O.rans_encode(t, 4096, d) for b, d in enumerate(datas))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shared_table_exchange_two_ranks_on_device():
+    """the int32 device histogram -> all_reduce -> k_tab
+    sequence of bench.py with two ranks (gloo, both on cuda:0): every rank's
+    streams equal the oracle's encoding under the union's table."""
+    import torch.multiprocessing as mp
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)

@@ -17,6 +17,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ran
 # 2. HBM traffic, one counter group per pass
 timeout -k 10 300 rocprofv3 $K --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o fetch -- $BP > $O/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 $K --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o write -- $BP > $O/pmc_write.log 2>&1
+# 2b. the literal configs[1] (one 256 MiB buffer, 4096 streams): trace + traffic
+L="python3 bench.py --buffers 1 --buffer-mib 256 --no-cpu-baseline --no-host-path"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/lit -o lit -- $L --steps 3 --warmup 1 > $O/lit_bench.log 2>&1
+timeout -k 10 300 rocprofv3 $K --pmc FETCH_SIZE --output-format csv -d $O/pmc_lit_fetch -o fetch -- $L --steps 1 --warmup 1 > $O/pmc_lit_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 $K --pmc WRITE_SIZE --output-format csv -d $O/pmc_lit_write -o write -- $L --steps 1 --warmup 1 > $O/pmc_lit_write.log 2>&1
 # 3. FSE workload (configs[2]) kernel trace + stats and traffic
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/fse -o fse -- python3 bench.py --workload fse --steps 5 --warmup 2 --no-cpu-baseline > $O/fse_bench.log 2>&1
 timeout -k 10 300 rocprofv3 $K --pmc FETCH_SIZE --output-format csv -d $O/pmc_fse_fetch -o fetch -- python3 bench.py --workload fse --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_fse_fetch.log 2>&1

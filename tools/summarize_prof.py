@@ -5,7 +5,8 @@ Prints per-kernel average duration (kernel-trace --stats) and per-dispatch HBM
 traffic from the PMC passes, corrected as MI355X_MICROARCH.md (HBM section)
 prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts
 half of the bytes of 16-B-per-lane streaming reads, so it is doubled. Writes
-<dir>/summary/traffic.json (kernel -> {fetch_bytes, write_bytes, hbm_bytes}).
+<dir>/summary/traffic.json ({"source", "workloads": {workload: {kernel: {fetch_bytes,
+write_bytes, hbm_bytes}}}}), the format bench.py reads from profiles/traffic.json.
 """
 import csv
 import glob
@@ -50,7 +51,8 @@ def main():
         for k, v in sorted(ks.items(), key=lambda kv: -kv[1]["pct"]):
             print(f"  {k:32s} calls={v['calls']:5d} avg={v['avg_us']:10.2f} us  {v['pct']:6.2f} %")
     traffic = {}
-    for tag, fsub, wsub in (("rans", "pmc_fetch", "pmc_write"), ("fse", "pmc_fse_fetch", "pmc_fse_write")):
+    for tag, fsub, wsub in (("rans", "pmc_fetch", "pmc_write"), ("rans_literal", "pmc_lit_fetch", "pmc_lit_write"),
+                            ("fse64", "pmc_fse_fetch", "pmc_fse_write")):
         fc, wc = counters(d, fsub), counters(d, wsub)
         ks = sorted({k for k, _ in fc} | {k for k, _ in wc})
         if ks:
@@ -58,11 +60,12 @@ def main():
         for k in ks:
             fb = fc.get((k, "FETCH_SIZE"), 0.0) * 1024 * 2
             wb = wc.get((k, "WRITE_SIZE"), 0.0) * 1024
-            traffic[k] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb, "workload": tag}
+            traffic.setdefault(tag, {})[k] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb}
             print(f"  {k:32s} fetch={fb / 1e6:10.2f} MB  write={wb / 1e6:10.2f} MB  total={(fb + wb) / 1e6:10.2f} MB")
     os.makedirs(os.path.join(d, "summary"), exist_ok=True)
     with open(os.path.join(d, "summary", "traffic.json"), "w") as fh:
-        json.dump(traffic, fh, indent=1)
+        json.dump({"source": os.path.basename(os.path.normpath(d)) + " PMC passes (FETCH_SIZE x2 + WRITE_SIZE)",
+                   "workloads": traffic}, fh, indent=1)
 
 
 if __name__ == "__main__":

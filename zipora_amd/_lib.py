@@ -8,6 +8,16 @@ import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libzipora_amd.so")
+# tools only: ZR_DIAG_LIB=1 loads the -DZR_DIAG build (profiling ablations that
+# read ZR_ABLATE / ZR_DEC_ABL / ZR_COMPACT_OLD); bench.py refuses to print a
+# metric line from it
+DIAG_LIB_PATH = os.path.join(_PKG, "libzipora_amd_diag.so")
+DIAG_ENV = ("ZR_DIAG_LIB", "ZR_ABLATE", "ZR_DEC_ABL", "ZR_COMPACT_OLD")
+
+
+def diag_env():
+    """The diagnostic switches set in this process's environment."""
+    return [k for k in DIAG_ENV if os.environ.get(k)]
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -62,6 +72,10 @@ SIGNATURES = [
                                         c_u8p, c_sz, ctypes.POINTER(c_sz)]),
     ("zr_rans_decode", ctypes.c_int32, [ctypes.POINTER(RansTable), ctypes.c_uint32, c_u8p, c_sz,
                                         c_u8p, c_sz]),
+    ("zr_rans_adaptive_streams", ctypes.c_uint32, [c_sz]),
+    ("zr_rans_encode_adaptive", ctypes.c_int32, [c_u8p, c_sz, c_u8p, c_sz, ctypes.POINTER(c_sz), c_u32p]),
+    ("zr_rans_selftest_reciprocal", ctypes.c_int32, [c_u64p]),
+    ("zr_device_alloc_count", ctypes.c_int32, [c_u64p]),
     ("zr_rans_dtab_bytes", c_sz, []),
     ("zr_rans_dtab_upload", ctypes.c_int32, [ctypes.POINTER(RansTable), ctypes.c_uint32, c_vp, c_vp]),
     ("zr_histogram_dev", ctypes.c_int32, [c_vp, ctypes.POINTER(RansBatch), ctypes.c_int32, c_vp, c_vp]),
@@ -179,13 +193,15 @@ def load(build_if_missing=True):
         import torch  # noqa: F401
     except Exception:
         pass
-    if not os.path.exists(LIB_PATH):
+    diag = bool(os.environ.get("ZR_DIAG_LIB"))
+    path = DIAG_LIB_PATH if diag else LIB_PATH
+    if not os.path.exists(path):
         if not build_if_missing:
-            raise RuntimeError(f"zipora_amd: HIP library missing at {LIB_PATH}; run "
+            raise RuntimeError(f"zipora_amd: HIP library missing at {path}; run "
                                "`python -m zipora_amd.build`")
         from . import build as _b
-        _b.build()
-    L = ctypes.CDLL(LIB_PATH)
+        _b.build(diag=diag)
+    L = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
         fn = getattr(L, name, None)
         if fn is None:

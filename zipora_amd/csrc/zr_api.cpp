@@ -1,8 +1,10 @@
 // zr_api.cpp -- host side of the C ABI: error state, table construction,
 // host-memory entry points, device helpers and synthetic inputs.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -21,6 +23,78 @@ int32_t set_error(int32_t code, const std::string &msg) {
     return code;
 }
 void clear_error() { g_last_error.clear(); }
+
+// ---------------------------------------------------------------- allocations
+static std::atomic<uint64_t> g_dev_allocs{0};
+
+hipError_t dev_alloc(void **p, size_t bytes) {
+    g_dev_allocs.fetch_add(1, std::memory_order_relaxed);
+    return hipMalloc(p, bytes ? bytes : 16);
+}
+
+// ---------------------------------------------------------------- call contexts
+namespace {
+std::mutex g_ctx_mx;
+std::map<int, std::vector<CallCtx *>> g_ctx_free;  // per device; contexts live for the process
+}  // namespace
+
+int32_t CallLease::acquire() {
+    int dev = 0;
+    ZR_HIP(hipGetDevice(&dev));
+    {
+        std::lock_guard<std::mutex> g(g_ctx_mx);
+        auto &v = g_ctx_free[dev];
+        if (!v.empty()) {
+            c_ = v.back();
+            v.pop_back();
+            return ZR_OK;
+        }
+    }
+    CallCtx *c = new CallCtx;
+    c->device = dev;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return set_error(ZR_INTERNAL, "hipStreamCreate failed");
+    }
+    c_ = c;
+    return ZR_OK;
+}
+
+CallLease::~CallLease() {
+    if (!c_) return;
+    (void)hipStreamSynchronize(c_->stream);  // nothing of this call may still run
+    std::lock_guard<std::mutex> g(g_ctx_mx);
+    g_ctx_free[c_->device].push_back(c_);
+}
+
+int32_t CallLease::get(int slot, size_t bytes, void **p) {
+    if (bytes == 0) bytes = 16;
+    if (bytes > c_->cap[slot]) {
+        // the stream is idle between calls and every call drains it before
+        // returning, so the old buffer is free; grow to the next power of two
+        // (at least 64 KiB) so that a run of growing calls reallocates rarely
+        size_t want = 64 << 10;
+        while (want < bytes) want <<= 1;
+        if (c_->buf[slot]) {
+            ZR_HIP(hipStreamSynchronize(c_->stream));
+            ZR_HIP(hipFree(c_->buf[slot]));
+            c_->buf[slot] = nullptr;
+            c_->cap[slot] = 0;
+        }
+        if (dev_alloc(&c_->buf[slot], want) != hipSuccess) {
+            c_->buf[slot] = nullptr;
+            return set_error(ZR_MEMORY_ERROR, "hipMalloc failed");
+        }
+        c_->cap[slot] = want;
+    }
+    *p = c_->buf[slot];
+    return ZR_OK;
+}
+
+int32_t CallLease::sync() {
+    ZR_HIP(hipStreamSynchronize(c_->stream));
+    return ZR_OK;
+}
 
 // ---------------------------------------------------------------- rANS table
 // Rans64Encoder::new (rans.rs:208-235) with normalize_frequencies (rans.rs:238-299).
@@ -86,9 +160,8 @@ void rans_dtab_from_table(const zr_rans_table *t, RansDTab *d) {
         const uint32_t f = t->freq[s];
         d->freq[s] = f;
         d->start[s] = t->start[s];
-        const uint32_t l = f <= 1 ? 0u : 32u - (uint32_t)__builtin_clz(f - 1);
-        d->rsh[s] = l;
-        d->rcp[s] = f ? (uint32_t)(((1ull << (24 + l)) + f - 1) / f) : 0u;
+        d->rsh[s] = enc_rsh(f);
+        d->rcp[s] = enc_rcp(f);
         if (f == TOTFREQ) single = true;
         for (uint32_t i = 0; i < f && t->start[s] + i < TOTFREQ; i++) {
             const uint32_t j = t->start[s] + i;
@@ -200,46 +273,54 @@ int32_t zr_rans_dtab_upload(const zr_rans_table *tables, uint32_t n_tables, void
                             void *stream) {
     ZR_GUARD_BEGIN
     clear_error();
-    std::vector<RansDTab> h(n_tables);
-    for (uint32_t i = 0; i < n_tables; i++) rans_dtab_from_table(&tables[i], &h[i]);
-    ZR_HIP(hipMemcpyAsync(dtabs_dev, h.data(), sizeof(RansDTab) * n_tables, hipMemcpyHostToDevice,
-                          (hipStream_t)stream));
-    ZR_HIP(hipStreamSynchronize((hipStream_t)stream));
+    if (n_tables == 0) return ZR_OK;
+    // the tables leave from a heap copy that a stream-ordered host callback
+    // frees after the copy (no host synchronisation)
+    auto *h = new std::vector<RansDTab>(n_tables);
+    for (uint32_t i = 0; i < n_tables; i++) rans_dtab_from_table(&tables[i], &(*h)[i]);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemcpyAsync(dtabs_dev, h->data(), sizeof(RansDTab) * n_tables, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+        delete h;
+        ZR_HIP(e);
+    }
+    ZR_HIP(hipLaunchHostFunc(
+        s, [](void *p) { delete static_cast<std::vector<RansDTab> *>(p); }, h));
     return ZR_OK;
     ZR_GUARD_END
 }
 
 // ---- host-memory rANS (synchronous; Rans64Encoder::encode / Rans64Decoder::decode)
 namespace {
-struct DevBuf {
-    void *p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-    hipError_t alloc(size_t n) { return hipMalloc(&p, n ? n : 16); }
-};
-
-// one-buffer batch run against device copies of the arguments
+// one-buffer batch run on a leased call context (no allocation in steady state,
+// synchronisation on the context's stream only)
 int32_t run_single(bool encode, const zr_rans_table *t, uint32_t N, const uint8_t *in, size_t in_len,
                    uint8_t *out, size_t out_cap, size_t n, size_t *out_len) {
     if (N == 0) N = 1;
     const size_t raw_len = encode ? in_len : n;
     const size_t enc_cap = encode ? zr_rans_encode_bound(in_len, N) : in_len;
-    DevBuf d_raw, d_enc, d_meta, d_tab, d_ws;
-    ZR_HIP(d_raw.alloc(raw_len));
-    ZR_HIP(d_enc.alloc(enc_cap));
-    ZR_HIP(d_meta.alloc(64));
-    ZR_HIP(d_tab.alloc(sizeof(RansDTab)));
+    CallLease L;
+    int32_t st = L.acquire();
+    if (st) return st;
+    void *d_raw, *d_enc, *d_meta, *d_tab, *d_ws;
     const size_t wsb = rans_workspace_bytes(1, N, raw_len);
-    ZR_HIP(d_ws.alloc(wsb));
-    RansDTab *h = new RansDTab;
+    if ((st = L.get(0, raw_len, &d_raw)) || (st = L.get(1, enc_cap, &d_enc)) || (st = L.get(2, 64, &d_meta)) ||
+        (st = L.get(3, sizeof(RansDTab), &d_tab)) || (st = L.get(4, wsb, &d_ws)))
+        return st;
+    CallCtx *c = L.ctx();
+    hipStream_t s = L.stream();
+    c->host_stage.resize(sizeof(RansDTab));
+    RansDTab *h = reinterpret_cast<RansDTab *>(&c->host_stage[0]);
     rans_dtab_from_table(t, h);
-    hipError_t e = hipMemcpy(d_tab.p, h, sizeof(RansDTab), hipMemcpyHostToDevice);
-    delete h;
-    ZR_HIP(e);
-    uint64_t meta[5] = {raw_len, 0, 0, encode ? 0 : (uint64_t)in_len, 0};
-    ZR_HIP(hipMemcpy(d_meta.p, meta, sizeof(meta), hipMemcpyHostToDevice));
-    uint64_t *m = reinterpret_cast<uint64_t *>(d_meta.p);
+    ZR_HIP(hipMemcpyAsync(d_tab, h, sizeof(RansDTab), hipMemcpyHostToDevice, s));
+    uint64_t *meta = c->meta;
+    meta[0] = raw_len;
+    meta[1] = 0;
+    meta[2] = 0;
+    meta[3] = encode ? 0 : (uint64_t)in_len;
+    meta[4] = 0;
+    ZR_HIP(hipMemcpyAsync(d_meta, meta, 5 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    uint64_t *m = reinterpret_cast<uint64_t *>(d_meta);
     zr_rans_batch bt;
     bt.n_buffers = 1;
     bt.n_streams = N;
@@ -249,20 +330,19 @@ int32_t run_single(bool encode, const zr_rans_table *t, uint32_t N, const uint8_
     bt.enc_off = m + 2;
     bt.enc_len = m + 3;
     bt.status = reinterpret_cast<int32_t *>(m + 4);
-    bt.tables = d_tab.p;
+    bt.tables = d_tab;
     bt.table_stride = 0;
     bt.min_len = raw_len;
-    int32_t st;
     if (encode) {
-        if (in_len) ZR_HIP(hipMemcpy(d_raw.p, in, in_len, hipMemcpyHostToDevice));
-        st = zr_rans_encode_batch_dev(&bt, (const uint8_t *)d_raw.p, (uint8_t *)d_enc.p, d_ws.p, wsb, nullptr);
+        if (in_len) ZR_HIP(hipMemcpyAsync(d_raw, in, in_len, hipMemcpyHostToDevice, s));
+        st = zr_rans_encode_batch_dev(&bt, (const uint8_t *)d_raw, (uint8_t *)d_enc, d_ws, wsb, s);
     } else {
-        if (in_len) ZR_HIP(hipMemcpy(d_enc.p, in, in_len, hipMemcpyHostToDevice));
-        st = zr_rans_decode_batch_dev(&bt, (const uint8_t *)d_enc.p, (uint8_t *)d_raw.p, d_ws.p, wsb, nullptr);
+        if (in_len) ZR_HIP(hipMemcpyAsync(d_enc, in, in_len, hipMemcpyHostToDevice, s));
+        st = zr_rans_decode_batch_dev(&bt, (const uint8_t *)d_enc, (uint8_t *)d_raw, d_ws, wsb, s);
     }
     if (st) return st;
-    ZR_HIP(hipDeviceSynchronize());
-    ZR_HIP(hipMemcpy(meta, d_meta.p, sizeof(meta), hipMemcpyDeviceToHost));
+    ZR_HIP(hipMemcpyAsync(meta, d_meta, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
     const int32_t status = (int32_t)(meta[4] & 0xFFFFFFFFu);
     if (status != 0) {
         if (encode) return set_error(ZR_INVALID_INPUT, "Symbol not in frequency table");
@@ -270,12 +350,12 @@ int32_t run_single(bool encode, const zr_rans_table *t, uint32_t N, const uint8_
     }
     if (encode) {
         if (meta[3] > out_cap) return set_error(ZR_INVALID_INPUT, "output capacity too small");
-        ZR_HIP(hipMemcpy(out, d_enc.p, meta[3], hipMemcpyDeviceToHost));
+        ZR_HIP(hipMemcpyAsync(out, d_enc, meta[3], hipMemcpyDeviceToHost, s));
         *out_len = meta[3];
     } else if (n) {
-        ZR_HIP(hipMemcpy(out, d_raw.p, n, hipMemcpyDeviceToHost));
+        ZR_HIP(hipMemcpyAsync(out, d_raw, n, hipMemcpyDeviceToHost, s));
     }
-    return ZR_OK;
+    return L.sync();
 }
 }  // namespace
 
@@ -299,10 +379,42 @@ int32_t zr_rans_decode(const zr_rans_table *t, uint32_t n_streams, const uint8_t
     ZR_GUARD_END
 }
 
+uint32_t zr_rans_adaptive_streams(size_t data_size) {
+    // AdaptiveRans64Encoder::select_variant (rans.rs:669-681)
+    if (data_size < 73) return 1;
+    if (data_size < 73ull * 73) return 2;
+    if (data_size < 73ull * 73 * 73 * 73) return 4;
+    return 8;
+}
+
+int32_t zr_rans_encode_adaptive(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap, size_t *out_len,
+                                uint32_t *n_streams) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if ((!in && n) || !out || !out_len) return set_error(ZR_INVALID_INPUT, "null argument");
+    // encode_adaptive (rans.rs:684-706): calculate_frequencies (:708-714, on
+    // the device), Rans64Encoder::<P>::new, encode with P = select_variant
+    uint32_t f[256];
+    int32_t st = zr_byte_histogram(in, n, f);
+    if (st) return st;
+    zr_rans_table t;
+    if ((st = rans_normalize_host(f, &t))) return st;
+    const uint32_t N = zr_rans_adaptive_streams(n);
+    if (n_streams) *n_streams = N;
+    return run_single(true, &t, N, in, n, out, out_cap, 0, out_len);
+    ZR_GUARD_END
+}
+
+int32_t zr_device_alloc_count(uint64_t *count) {
+    if (!count) return set_error(ZR_INVALID_INPUT, "null argument");
+    *count = g_dev_allocs.load(std::memory_order_relaxed);
+    return ZR_OK;
+}
+
 // ---- device helpers
 int32_t zr_malloc_dev(void **ptr, size_t bytes) {
     ZR_GUARD_BEGIN
-    hipError_t e = hipMalloc(ptr, bytes ? bytes : 16);
+    hipError_t e = dev_alloc(ptr, bytes);
     if (e != hipSuccess) return set_error(ZR_MEMORY_ERROR, "hipMalloc failed");
     return ZR_OK;
     ZR_GUARD_END

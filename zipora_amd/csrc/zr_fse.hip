@@ -1076,15 +1076,8 @@ int32_t zr_fse_decompress_dev(const uint8_t *in, size_t n, uint8_t *out, size_t 
     ZR_GUARD_END
 }
 
-// ---- host-memory entry points (synchronous)
-namespace {
-struct DBuf {
-    void *p = nullptr;
-    ~DBuf() {
-        if (p) (void)hipFree(p);
-    }
-};
-}  // namespace
+// ---- host-memory entry points (synchronous, on a leased call context:
+// zr_internal.h CallLease -- no allocation in steady state, stream-scoped sync)
 
 int32_t zr_fse_decompressed_size(const uint8_t *in, size_t n, size_t *out_len) {
     ZR_GUARD_BEGIN
@@ -1125,16 +1118,19 @@ int32_t zr_byte_histogram(const uint8_t *in, size_t n, uint32_t freqs[256]) {
     clear_error();
     memset(freqs, 0, 1024);
     if (n == 0) return ZR_OK;
-    DBuf din, dh;
-    ZR_HIP(hipMalloc(&din.p, n));
-    ZR_HIP(hipMalloc(&dh.p, 1024));
-    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
-    ZR_HIP(hipMemset(dh.p, 0, 1024));
-    hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, FH_CHUNK)), dim3(256), 0, nullptr,
-                       (const uint8_t *)din.p, (uint64_t)n, (uint32_t *)dh.p);
+    CallLease L;
+    int32_t st = L.acquire();
+    if (st) return st;
+    void *din, *dh;
+    if ((st = L.get(0, n, &din)) || (st = L.get(2, 1024, &dh))) return st;
+    hipStream_t s = L.stream();
+    ZR_HIP(hipMemcpyAsync(din, in, n, hipMemcpyHostToDevice, s));
+    ZR_HIP(hipMemsetAsync(dh, 0, 1024, s));
+    hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, FH_CHUNK)), dim3(256), 0, s, (const uint8_t *)din,
+                       (uint64_t)n, (uint32_t *)dh);
     ZR_HIP(hipGetLastError());
-    ZR_HIP(hipMemcpy(freqs, dh.p, 1024, hipMemcpyDeviceToHost));
-    return ZR_OK;
+    ZR_HIP(hipMemcpyAsync(freqs, dh, 1024, hipMemcpyDeviceToHost, s));
+    return L.sync();
     ZR_GUARD_END
 }
 
@@ -1147,28 +1143,32 @@ int32_t zr_fse_compress_freqs(const zr_fse_config *c, const uint32_t *freqs, con
     *out_len = 0;
     if (n == 0) return ZR_OK;
     const size_t wsb = zr_fse_workspace_bytes(n, c), cap = zr_fse_compress_bound(n, c);
-    DBuf din, dout, dws, dm;
-    ZR_HIP(hipMalloc(&din.p, n));
-    ZR_HIP(hipMalloc(&dout.p, cap));
-    ZR_HIP(hipMalloc(&dws.p, wsb));
-    ZR_HIP(hipMalloc(&dm.p, 64 + 1024));
-    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
-    uint64_t *olen = reinterpret_cast<uint64_t *>(dm.p);
+    CallLease L;
+    if ((st = L.acquire())) return st;
+    void *din, *dout, *dws, *dm;
+    if ((st = L.get(0, n, &din)) || (st = L.get(1, cap, &dout)) || (st = L.get(4, wsb, &dws)) ||
+        (st = L.get(2, 64 + 1024, &dm)))
+        return st;
+    hipStream_t s = L.stream();
+    CallCtx *cx = L.ctx();
+    ZR_HIP(hipMemcpyAsync(din, in, n, hipMemcpyHostToDevice, s));
+    uint64_t *olen = reinterpret_cast<uint64_t *>(dm);
     int32_t *dst = reinterpret_cast<int32_t *>(olen + 1);
     uint32_t *dfreq = nullptr;
     if (freqs) {
-        dfreq = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(dm.p) + 64);
-        ZR_HIP(hipMemcpy(dfreq, freqs, 1024, hipMemcpyHostToDevice));
+        dfreq = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(dm) + 64);
+        cx->host_stage.assign(reinterpret_cast<const char *>(freqs), 1024);
+        ZR_HIP(hipMemcpyAsync(dfreq, cx->host_stage.data(), 1024, hipMemcpyHostToDevice, s));
     }
-    st = zr_fse_compress_dev(c, dfreq, (const uint8_t *)din.p, n, (uint8_t *)dout.p, olen, dst, dws.p, wsb,
-                             nullptr);
+    st = zr_fse_compress_dev(c, dfreq, (const uint8_t *)din, n, (uint8_t *)dout, olen, dst, dws, wsb, s);
     if (st) return st;
-    ZR_HIP(hipDeviceSynchronize());
-    uint64_t meta[2];
-    ZR_HIP(hipMemcpy(meta, dm.p, 16, hipMemcpyDeviceToHost));
+    uint64_t *meta = cx->meta;
+    ZR_HIP(hipMemcpyAsync(meta, dm, 16, hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
     if ((int32_t)meta[1] != 0) return set_error(ZR_INVALID_INPUT, "FSE compression failed");
     if (meta[0] > out_cap) return set_error(ZR_INVALID_INPUT, "output capacity too small");
-    ZR_HIP(hipMemcpy(out, dout.p, meta[0], hipMemcpyDeviceToHost));
+    ZR_HIP(hipMemcpyAsync(out, dout, meta[0], hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
     *out_len = meta[0];
     return ZR_OK;
     ZR_GUARD_END
@@ -1186,22 +1186,25 @@ int32_t zr_fse_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_
         if (nb <= (n - 5) / 4 && nb > 0) maxb = nb;
     }
     const size_t wsb = fse_dec_ws_bytes(maxb);
-    DBuf din, dout, dws, dm;
-    ZR_HIP(hipMalloc(&din.p, n));
-    ZR_HIP(hipMalloc(&dout.p, out_cap ? out_cap : 16));
-    ZR_HIP(hipMalloc(&dws.p, wsb));
-    ZR_HIP(hipMalloc(&dm.p, 64));
-    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
-    uint64_t *olen = reinterpret_cast<uint64_t *>(dm.p);
-    int32_t *dst = reinterpret_cast<int32_t *>(olen + 1);
-    int32_t st = zr_fse_decompress_dev((const uint8_t *)din.p, n, (uint8_t *)dout.p, out_cap, maxb, olen, dst,
-                                       dws.p, wsb, nullptr);
+    CallLease L;
+    int32_t st = L.acquire();
     if (st) return st;
-    ZR_HIP(hipDeviceSynchronize());
-    uint64_t meta[2];
-    ZR_HIP(hipMemcpy(meta, dm.p, 16, hipMemcpyDeviceToHost));
+    void *din, *dout, *dws, *dm;
+    if ((st = L.get(0, n, &din)) || (st = L.get(1, out_cap, &dout)) || (st = L.get(4, wsb, &dws)) ||
+        (st = L.get(2, 64, &dm)))
+        return st;
+    hipStream_t s = L.stream();
+    ZR_HIP(hipMemcpyAsync(din, in, n, hipMemcpyHostToDevice, s));
+    uint64_t *olen = reinterpret_cast<uint64_t *>(dm);
+    int32_t *dst = reinterpret_cast<int32_t *>(olen + 1);
+    st = zr_fse_decompress_dev((const uint8_t *)din, n, (uint8_t *)dout, out_cap, maxb, olen, dst, dws, wsb, s);
+    if (st) return st;
+    uint64_t *meta = L.ctx()->meta;
+    ZR_HIP(hipMemcpyAsync(meta, dm, 16, hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
     if ((int32_t)meta[1] != 0) return set_error((int32_t)meta[1], "FSE decompression failed: invalid data");
-    if (meta[0]) ZR_HIP(hipMemcpy(out, dout.p, meta[0], hipMemcpyDeviceToHost));
+    if (meta[0]) ZR_HIP(hipMemcpyAsync(out, dout, meta[0], hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
     *out_len = meta[0];
     return ZR_OK;
     ZR_GUARD_END

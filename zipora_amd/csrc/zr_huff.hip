@@ -445,7 +445,21 @@ __device__ uint64_t seg_decode(const HuffDecArgs &a, uint64_t p, uint64_t lim, u
     return c;
 }
 
-__global__ __launch_bounds__(256) void k_huff_seg(HuffDecArgs a) {
+// Segment synchronisation runs entirely on the device (no host round trip):
+// round r re-decodes the dirty segments, then moves every start to the end of
+// the previous segment and records in changed[r] whether any start moved.
+// Round r > 0 does nothing once round r-1 changed nothing (converged).
+__global__ __launch_bounds__(256) void k_huff_init(HuffDecArgs a, uint32_t nflags) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < a.nseg) {
+        a.start[t] = t * HD_SEG;  // the guessed boundaries
+        a.dirty[t] = 1;
+    }
+    if (t < nflags) a.changed[t] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_huff_seg(HuffDecArgs a, uint32_t round) {
+    if (round > 0 && a.changed[round - 1] == 0) return;
     const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= a.nseg || !a.dirty[t]) return;
     const uint64_t lim = min((t + 1) * HD_SEG, a.B);
@@ -455,15 +469,40 @@ __global__ __launch_bounds__(256) void k_huff_seg(HuffDecArgs a) {
     a.dirty[t] = 0;
 }
 
-__global__ __launch_bounds__(256) void k_huff_fix(HuffDecArgs a) {
+__global__ __launch_bounds__(256) void k_huff_fix(HuffDecArgs a, uint32_t round) {
+    if (round > 0 && a.changed[round - 1] == 0) return;
     const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (t == 0 || t >= a.nseg) return;
     const uint64_t s = a.end[t - 1];
     if (s != a.start[t]) {
         a.start[t] = s;
         a.dirty[t] = 1;
-        *a.changed = 1;
+        a.changed[round] = 1;
     }
+}
+
+// After the parallel rounds: if the last round still moved a start, resolve
+// the rest in order on one thread (exact, O(stream) -- only for streams whose
+// wrong guesses did not resynchronise within the rounds).
+__global__ void k_huff_serial(HuffDecArgs a, uint32_t last) {
+    if (a.changed[last] == 0 || threadIdx.x != 0) return;
+    for (uint64_t t = 0; t < a.nseg; t++) {
+        if (t > 0 && a.end[t - 1] != a.start[t]) {
+            a.start[t] = a.end[t - 1];
+            a.dirty[t] = 1;
+        }
+        if (a.dirty[t]) {
+            uint64_t pe;
+            a.cnt[t] = seg_decode<false>(a, a.start[t], min((t + 1) * HD_SEG, a.B), &pe, 0);
+            a.end[t] = pe;
+            a.dirty[t] = 0;
+        }
+    }
+}
+
+// fewer complete codes than requested (decoder.rs:157-163)
+__global__ void k_huff_check(const uint64_t *total, uint64_t n, int32_t *status) {
+    if (threadIdx.x == 0 && *total < n) *status = ZR_INVALID_INPUT;
 }
 
 __global__ __launch_bounds__(256) void k_huff_write(HuffDecArgs a) {
@@ -745,49 +784,34 @@ int32_t zr_huff_decode_dev(const zr_huff_tree *t, const uint8_t *in, size_t in_l
     a.n = n;
     ZR_HIP(hipMemsetAsync(stream_copy + in_len, 0, 64, s));
     launch_copy(in, stream_copy, in_len, s);
-    ZR_HIP(hipMemcpyAsync(dlut, lut.data(), lut.size() * 4, hipMemcpyHostToDevice, s));
-    // segment starts: the guessed boundaries t * SEG
-    std::vector<uint64_t> st0(nseg);
-    for (uint64_t i = 0; i < nseg; i++) st0[i] = i * HD_SEG;
-    ZR_HIP(hipMemcpyAsync(a.start, st0.data(), 8 * nseg, hipMemcpyHostToDevice, s));
-    ZR_HIP(hipMemsetAsync(a.dirty, 1, nseg, s));
+    // the decode table leaves from a heap copy that a stream-ordered host
+    // callback frees once the copy has run (no host synchronisation here)
+    auto *held = new std::vector<uint32_t>(std::move(lut));
+    ZR_HIP(hipMemcpyAsync(dlut, held->data(), held->size() * 4, hipMemcpyHostToDevice, s));
+    ZR_HIP(hipLaunchHostFunc(
+        s, [](void *p) { delete static_cast<std::vector<uint32_t> *>(p); }, held));
     const uint32_t g = (uint32_t)ceil_div(nseg, 256);
+    constexpr uint32_t ROUNDS = 4;  // chain and fixed-length codes settle in 1-2
+    hipLaunchKernelGGL(k_huff_init, dim3(g), dim3(256), 0, s, a, ROUNDS);
     timer_begin("huff_decode", s);
-    for (uint64_t it = 0; it <= nseg + 1; it++) {
-        hipLaunchKernelGGL(k_huff_seg, dim3(g), dim3(256), 0, s, a);
-        ZR_HIP(hipMemsetAsync(flag, 0, 4, s));
-        hipLaunchKernelGGL(k_huff_fix, dim3(g), dim3(256), 0, s, a);
-        uint32_t changed = 0;
-        ZR_HIP(hipMemcpyAsync(&changed, flag, 4, hipMemcpyDeviceToHost, s));
-        ZR_HIP(hipStreamSynchronize(s));
-        if (!changed) break;
+    for (uint32_t r = 0; r < ROUNDS; r++) {
+        hipLaunchKernelGGL(k_huff_seg, dim3(g), dim3(256), 0, s, a, r);
+        hipLaunchKernelGGL(k_huff_fix, dim3(g), dim3(256), 0, s, a, r);
     }
-    uint64_t *tot = reinterpret_cast<uint64_t *>(flag + 2);
+    hipLaunchKernelGGL(k_huff_serial, dim3(1), dim3(64), 0, s, a, ROUNDS - 1);
+    uint64_t *tot = reinterpret_cast<uint64_t *>(flag + 8);
     hipLaunchKernelGGL(k_huff_scan, dim3(1), dim3(256), 0, s, a.cnt, nseg, tot, (uint64_t *)nullptr,
                        (const int32_t *)nullptr);
     hipLaunchKernelGGL(k_huff_write, dim3(g), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_huff_check, dim3(1), dim3(64), 0, s, (const uint64_t *)tot, (uint64_t)n, status_dev);
     timer_end("huff_decode", s);
-    uint64_t total = 0;
-    ZR_HIP(hipMemcpyAsync(&total, tot, 8, hipMemcpyDeviceToHost, s));
-    ZR_HIP(hipStreamSynchronize(s));
-    if (total < n) {  // fewer complete codes than requested (decoder.rs:157-163)
-        const int32_t bad = ZR_INVALID_INPUT;
-        ZR_HIP(hipMemcpy(status_dev, &bad, 4, hipMemcpyHostToDevice));
-        return set_error(ZR_INVALID_INPUT, "Decoded length mismatch");
-    }
+    ZR_HIP(hipGetLastError());
     return ZR_OK;
     ZR_GUARD_END
 }
 
-namespace {
-struct DMem {
-    void *p = nullptr;
-    ~DMem() {
-        if (p) (void)hipFree(p);
-    }
-};
-}  // namespace
-
+// ---- host-memory entry points (synchronous, on a leased call context:
+// zr_internal.h CallLease -- no allocation in steady state, stream-scoped sync)
 int32_t zr_huff_encode(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
                        size_t *out_len) {
     ZR_GUARD_BEGIN
@@ -795,23 +819,26 @@ int32_t zr_huff_encode(const zr_huff_tree *t, const uint8_t *in, size_t n, uint8
     *out_len = 0;
     if (n == 0) return ZR_OK;
     const size_t wsb = zr_huff_workspace_bytes(n, 0), cap = zr_huff_encode_bound(t, n);
-    DMem din, dout, dws, dm;
-    ZR_HIP(hipMalloc(&din.p, n));
-    ZR_HIP(hipMalloc(&dout.p, cap));
-    ZR_HIP(hipMalloc(&dws.p, wsb));
-    ZR_HIP(hipMalloc(&dm.p, 64));
-    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
-    uint64_t *olen = reinterpret_cast<uint64_t *>(dm.p);
-    int32_t *dst = reinterpret_cast<int32_t *>(olen + 1);
-    int32_t st = zr_huff_encode_dev(t, (const uint8_t *)din.p, n, (uint8_t *)dout.p, cap, olen, dst, dws.p, wsb,
-                                    nullptr);
+    CallLease L;
+    int32_t st = L.acquire();
     if (st) return st;
-    ZR_HIP(hipDeviceSynchronize());
-    uint64_t meta[2];
-    ZR_HIP(hipMemcpy(meta, dm.p, 16, hipMemcpyDeviceToHost));
+    void *din, *dout, *dws, *dm;
+    if ((st = L.get(0, n, &din)) || (st = L.get(1, cap, &dout)) || (st = L.get(4, wsb, &dws)) ||
+        (st = L.get(2, 64, &dm)))
+        return st;
+    hipStream_t s = L.stream();
+    ZR_HIP(hipMemcpyAsync(din, in, n, hipMemcpyHostToDevice, s));
+    uint64_t *olen = reinterpret_cast<uint64_t *>(dm);
+    int32_t *dst = reinterpret_cast<int32_t *>(olen + 1);
+    st = zr_huff_encode_dev(t, (const uint8_t *)din, n, (uint8_t *)dout, cap, olen, dst, dws, wsb, s);
+    if (st) return st;
+    uint64_t *meta = L.ctx()->meta;
+    ZR_HIP(hipMemcpyAsync(meta, dm, 16, hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
     if ((int32_t)meta[1]) return set_error(ZR_INVALID_INPUT, "Symbol not in Huffman tree");
     if (meta[0] > out_cap) return set_error(ZR_INVALID_INPUT, "output capacity too small");
-    ZR_HIP(hipMemcpy(out, dout.p, meta[0], hipMemcpyDeviceToHost));
+    ZR_HIP(hipMemcpyAsync(out, dout, meta[0], hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
     *out_len = meta[0];
     return ZR_OK;
     ZR_GUARD_END
@@ -822,19 +849,41 @@ int32_t zr_huff_decode(const zr_huff_tree *t, const uint8_t *in, size_t in_len, 
     clear_error();
     if (in_len == 0 || n == 0) return ZR_OK;
     const size_t wsb = zr_huff_workspace_bytes(0, in_len);
-    DMem din, dout, dws, dm;
-    ZR_HIP(hipMalloc(&din.p, in_len));
-    ZR_HIP(hipMalloc(&dout.p, n));
-    ZR_HIP(hipMalloc(&dws.p, wsb));
-    ZR_HIP(hipMalloc(&dm.p, 64));
-    ZR_HIP(hipMemcpy(din.p, in, in_len, hipMemcpyHostToDevice));
-    int32_t st = zr_huff_decode_dev(t, (const uint8_t *)din.p, in_len, (uint8_t *)dout.p, n, (int32_t *)dm.p,
-                                    dws.p, wsb, nullptr);
+    CallLease L;
+    int32_t st = L.acquire();
     if (st) return st;
-    ZR_HIP(hipDeviceSynchronize());
-    ZR_HIP(hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
-    return ZR_OK;
+    void *din, *dout, *dws, *dm;
+    if ((st = L.get(0, in_len, &din)) || (st = L.get(1, n, &dout)) || (st = L.get(4, wsb, &dws)) ||
+        (st = L.get(2, 64, &dm)))
+        return st;
+    hipStream_t s = L.stream();
+    ZR_HIP(hipMemcpyAsync(din, in, in_len, hipMemcpyHostToDevice, s));
+    st = zr_huff_decode_dev(t, (const uint8_t *)din, in_len, (uint8_t *)dout, n, (int32_t *)dm, dws, wsb, s);
+    if (st) return st;
+    uint64_t *meta = L.ctx()->meta;
+    ZR_HIP(hipMemcpyAsync(meta, dm, 8, hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
+    if ((int32_t)meta[0] != 0) return set_error(ZR_INVALID_INPUT, "Decoded length mismatch");
+    ZR_HIP(hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, s));
+    return L.sync();
     ZR_GUARD_END
+}
+
+// order-1/2 host calls: the identity / transpose kernels on a leased context
+static int32_t ctx_host_run(const zr_ctx_huff *h, int32_t nway, bool enc, const uint8_t *in, size_t in_len,
+                            uint8_t *out, size_t n) {
+    CallLease L;
+    int32_t st = L.acquire();
+    if (st) return st;
+    void *din, *dout;
+    if ((st = L.get(0, in_len, &din)) || (st = L.get(1, n, &dout))) return st;
+    hipStream_t s = L.stream();
+    ZR_HIP(hipMemcpyAsync(din, in, in_len, hipMemcpyHostToDevice, s));
+    st = enc ? zr_ctx_huff_encode_dev(h, nway, (const uint8_t *)din, n, (uint8_t *)dout, s)
+             : zr_ctx_huff_decode_dev(h, nway, (const uint8_t *)din, in_len, (uint8_t *)dout, n, s);
+    if (st) return st;
+    ZR_HIP(hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, s));
+    return L.sync();
 }
 
 // ---------------------------------------------------------- contextual O1/O2
@@ -957,14 +1006,8 @@ int32_t zr_ctx_huff_encode(const zr_ctx_huff *h, int32_t nway, const uint8_t *in
         return set_error(ZR_INVALID_INPUT, "Interleaving only supported for Order-1 Huffman encoding");
     if (n == 0) return ZR_OK;
     if (out_cap < n) return set_error(ZR_INVALID_INPUT, "output capacity too small");
-    DMem din, dout;
-    ZR_HIP(hipMalloc(&din.p, n));
-    ZR_HIP(hipMalloc(&dout.p, n));
-    ZR_HIP(hipMemcpy(din.p, in, n, hipMemcpyHostToDevice));
-    int32_t st = zr_ctx_huff_encode_dev(h, nway, (const uint8_t *)din.p, n, (uint8_t *)dout.p, nullptr);
+    int32_t st = ctx_host_run(h, nway, true, in, n, out, n);
     if (st) return st;
-    ZR_HIP(hipDeviceSynchronize());
-    ZR_HIP(hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
     *out_len = n;
     return ZR_OK;
     ZR_GUARD_END
@@ -991,14 +1034,8 @@ int32_t zr_ctx_huff_decode(const zr_ctx_huff *h, int32_t nway, const uint8_t *in
         return set_error(ZR_INVALID_INPUT, "Interleaving only supported for Order-1 Huffman decoding");
     if (in_len == 0 || n == 0) return ZR_OK;
     if (in_len < n) return set_error(ZR_INVALID_INPUT, "Decoded length mismatch");
-    DMem din, dout;
-    ZR_HIP(hipMalloc(&din.p, in_len));
-    ZR_HIP(hipMalloc(&dout.p, n));
-    ZR_HIP(hipMemcpy(din.p, in, in_len, hipMemcpyHostToDevice));
-    int32_t st = zr_ctx_huff_decode_dev(h, nway, (const uint8_t *)din.p, in_len, (uint8_t *)dout.p, n, nullptr);
+    int32_t st = ctx_host_run(h, nway, false, in, in_len, out, n);
     if (st) return st;
-    ZR_HIP(hipDeviceSynchronize());
-    ZR_HIP(hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
     *out_len = n;
     return ZR_OK;
     ZR_GUARD_END

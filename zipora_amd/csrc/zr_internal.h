@@ -56,6 +56,19 @@ struct alignas(16) RansDTab {
     uint32_t slot[TOTFREQ];
 };
 
+// Encoder division x / freq for x < 2^24 (rans.rs:331 with the state in
+// [2^16, 2^24)): q = umulhi(x << 8, rcp) >> rsh, Granlund-Montgomery with
+// N = 24, l = ceil(log2 freq), rcp = ceil(2^(24+l) / freq). Shared by the
+// device table build (k_tab), the host table build and the exhaustive
+// self-test (zr_rans_selftest_reciprocal).
+__host__ __device__ inline uint32_t enc_rsh(uint32_t f) { return f <= 1 ? 0u : 32u - (uint32_t)__builtin_clz(f - 1); }
+__host__ __device__ inline uint32_t enc_rcp(uint32_t f) {
+    return f ? (uint32_t)(((1ull << (24 + enc_rsh(f))) + f - 1) / f) : 0u;
+}
+__host__ __device__ inline uint32_t enc_div(uint32_t x, uint32_t rcp, uint32_t rsh) {
+    return (uint32_t)(((uint64_t)(x << 8) * rcp) >> 32) >> rsh;
+}
+
 // host-side Rans64Encoder::new restatement (used by zr_rans_table_build and dtab upload)
 int32_t rans_normalize_host(const uint32_t raw[256], zr_rans_table *out);
 void rans_dtab_from_table(const zr_rans_table *t, RansDTab *d);
@@ -82,4 +95,45 @@ void timer_end(const char *name, hipStream_t s);
 
 inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 inline uint64_t round_up(uint64_t a, uint64_t b) { return ceil_div(a, b) * b; }
+
+// Every device allocation the library makes goes through dev_alloc, which
+// counts it (zr_device_alloc_count): the synchronous host entry points must
+// reach a steady state with no allocation per call.
+hipError_t dev_alloc(void **p, size_t bytes);
+
+// ---------------------------------------------------------------------------
+// Call contexts of the synchronous host-memory entry points (zr_rans_encode,
+// zr_fse_compress, zr_huff_decode, ...): a non-blocking HIP stream plus device
+// buffers grown on demand and kept. A call leases a context from a per-device
+// pool and returns it, so concurrent host threads never share one, the only
+// synchronisation is on the context's own stream (never the device), and once
+// the sizes have been seen a call allocates nothing.
+// ---------------------------------------------------------------------------
+struct CallCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    enum { NBUF = 6 };
+    void *buf[NBUF] = {};
+    size_t cap[NBUF] = {};
+    // host-side staging that must outlive the asynchronous copies of a call
+    alignas(16) uint64_t meta[16] = {};
+    std::string host_stage;
+};
+
+class CallLease {
+   public:
+    CallLease() = default;
+    CallLease(const CallLease &) = delete;
+    CallLease &operator=(const CallLease &) = delete;
+    ~CallLease();  // drains the stream, returns the context to the pool
+    int32_t acquire();
+    // device buffer `slot` with at least `bytes` bytes (grown, never shrunk)
+    int32_t get(int slot, size_t bytes, void **p);
+    hipStream_t stream() const { return c_->stream; }
+    CallCtx *ctx() { return c_; }
+    int32_t sync();
+
+   private:
+    CallCtx *c_ = nullptr;
+};
 }  // namespace zr

@@ -128,7 +128,7 @@ int32_t grow(void **p, size_t *cap, size_t need) {
     if (*p) ZR_HIP(hipFree(*p));
     *p = nullptr;
     *cap = 0;
-    ZR_HIP(hipMalloc(p, need));
+    ZR_HIP(dev_alloc(p, need));
     *cap = need;
     return ZR_OK;
 }
@@ -139,7 +139,7 @@ int32_t slot_meta(Slot &S, uint32_t nb) {
     if (S.hmeta) ZR_HIP(hipHostFree(S.hmeta));
     S.meta = nullptr;
     S.hmeta = nullptr;
-    ZR_HIP(hipMalloc(reinterpret_cast<void **>(&S.meta), meta_bytes(nb)));
+    ZR_HIP(dev_alloc(reinterpret_cast<void **>(&S.meta), meta_bytes(nb)));
     ZR_HIP(hipHostMalloc(reinterpret_cast<void **>(&S.hmeta), meta_bytes(nb),
                          hipHostMallocMapped | hipHostMallocCoherent));
     ZR_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&S.hmeta_dev), S.hmeta, 0));
@@ -243,9 +243,9 @@ struct Packed {
     uint64_t pos = 0;
 };
 
-int32_t run(zr_rans_pipe *p, bool encode, uint32_t B, const uint64_t *len, uint8_t *raw,
-            const uint64_t *raw_off, uint8_t *enc, const uint64_t *enc_off, uint64_t *enc_len,
-            int32_t *status, Packed *pk = nullptr) {
+int32_t run_impl(zr_rans_pipe *p, bool encode, uint32_t B, const uint64_t *len, uint8_t *raw,
+                 const uint64_t *raw_off, uint8_t *enc, const uint64_t *enc_off, uint64_t *enc_len,
+                 int32_t *status, Packed *pk) {
     const uint32_t N = p->N;
     const auto gs = groups(len, B, p->group_cap);
     Trace tr;
@@ -411,6 +411,25 @@ int32_t run(zr_rans_pipe *p, bool encode, uint32_t B, const uint64_t *len, uint8
     return ZR_OK;
 }
 
+// Any error return leaves copies in flight on the three streams and slots
+// marked busy with this call's group geometry. Drain every stream before
+// returning (no copy may land in caller memory after the error is reported)
+// and forget the slots, so the next call starts clean.
+int32_t run(zr_rans_pipe *p, bool encode, uint32_t B, const uint64_t *len, uint8_t *raw, const uint64_t *raw_off,
+            uint8_t *enc, const uint64_t *enc_off, uint64_t *enc_len, int32_t *status, Packed *pk = nullptr) {
+    const int32_t st = run_impl(p, encode, B, len, raw, raw_off, enc, enc_off, enc_len, status, pk);
+    if (st != ZR_OK) {
+        (void)hipStreamSynchronize(p->s_in);
+        (void)hipStreamSynchronize(p->s_cmp);
+        (void)hipStreamSynchronize(p->s_out);
+        for (Slot &S : p->slot) {
+            S.busy = false;
+            S.b0 = S.nb = 0;
+        }
+    }
+    return st;
+}
+
 void release(zr_rans_pipe *p) {
     for (Slot &S : p->slot) {
         if (S.raw) (void)hipFree(S.raw);
@@ -458,7 +477,7 @@ int32_t zr_rans_pipe_create(const zr_rans_table *table, uint32_t n_streams, uint
             hipEventCreateWithFlags(&S.out_done, hipEventDisableTiming) != hipSuccess)
             return fail(set_error(ZR_INTERNAL, "hipEventCreate failed"));
     }
-    if (hipMalloc(&p->dtab, zr_rans_dtab_bytes()) != hipSuccess)
+    if (dev_alloc(&p->dtab, zr_rans_dtab_bytes()) != hipSuccess)
         return fail(set_error(ZR_MEMORY_ERROR, "hipMalloc failed"));
     int32_t st = zr_rans_dtab_upload(table, 1, p->dtab, p->s_cmp);
     if (st) return fail(st);

@@ -63,6 +63,13 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v, unsigned long long *sh
     return t;
 }
 
+// sum over one wave (every lane gets it)
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor((unsigned long long)v, d, 64);
+    return v;
+}
+
 __device__ __forceinline__ const RansDTab *tab_for(const void *tables, uint32_t stride, uint32_t b) {
     return reinterpret_cast<const RansDTab *>(tables) + (size_t)stride * b;
 }
@@ -247,9 +254,15 @@ __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tab
     // pass 1: one slot per present symbol (rans.rs:244-250)
     const uint32_t used = (uint32_t)block_sum(f > 0, sh);
     const uint64_t ir = TOTFREQ - used;  // initial_remaining (rans.rs:263)
-    // pass 2: proportional share of the initial budget (rans.rs:264-271). The
-    // min(remaining) clamp never binds because sum(f*ir/total) <= ir.
-    uint32_t add = f > 0 ? (uint32_t)(((uint64_t)f * ir) / (uint64_t)total) : 0;
+    // pass 2: proportional share of the initial budget (rans.rs:264-271),
+    // additional = (f * ir / total) as u32, clamped to the live `remaining`.
+    // The sequential loop's remaining before symbol v is max(ir - P_v, 0) with
+    // P_v the exclusive prefix sum of the unclamped shares (once it hits 0 it
+    // stays 0), so to_add_v = min(add_v, ir - min(P_v, ir)). The clamp binds
+    // when the u32 total of rans.rs:209 has wrapped (sum of counts >= 2^32).
+    const uint32_t add_raw = f > 0 ? (uint32_t)(((uint64_t)f * ir) / (uint64_t)total) : 0;
+    const uint64_t pre_add = block_excl_scan(add_raw, sh, nullptr);
+    const uint32_t add = (uint32_t)min((uint64_t)add_raw, ir - min(pre_add, ir));
     uint32_t norm = (f > 0 ? 1u : 0u) + add;
     uint32_t remaining = (uint32_t)(ir - block_sum(add, sh));
     norm_s[v] = norm;
@@ -288,9 +301,8 @@ __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tab
     start_s[v] = start;
     d->freq[v] = norm;
     d->start[v] = start;
-    uint32_t l = norm <= 1 ? 0u : 32u - __clz(norm - 1);
-    d->rsh[v] = l;
-    d->rcp[v] = norm ? (uint32_t)(((1ull << (24 + l)) + norm - 1) / norm) : 0u;
+    d->rsh[v] = enc_rsh(norm);
+    d->rcp[v] = enc_rcp(norm);
     const uint32_t maxn = (uint32_t)__syncthreads_or(norm == TOTFREQ);
     __syncthreads();
     // slot owners: mark each present symbol's start, then a max-scan over the
@@ -371,9 +383,14 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 // ======================================================================
 // encode, xN layout: one lane per stream (rans.rs:369-420, encode_symbol :303-335)
 // ======================================================================
-__global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w, int ablate) {
-    const uint32_t nblk = w.nblk;
-    const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+// EW: workgroup width = streams per workgroup (256; 64 spreads a batch of few
+// streams, e.g. one buffer x 4096, over as many CUs as it has waves).
+// ABL: diagnostic ablations, ZR_DIAG builds only (1: no scratch stores,
+// 2: conflict-free table reads); the product instantiates ABL = 0.
+template <uint32_t EW, int ABL>
+__global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
+    const uint32_t nblkE = (a.N + EW - 1) / EW;
+    const uint32_t b = blockIdx.x / nblkE, blk = blockIdx.x % nblkE;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
@@ -388,36 +405,37 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     __shared__ uint4 et[256];
     __shared__ unsigned long long sh[4];
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
-    {
-        const uint32_t v = threadIdx.x, f = T->freq[v];
+    for (uint32_t v = threadIdx.x; v < 256; v += EW) {
+        const uint32_t f = T->freq[v];
         const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
         et[v] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
                            (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
     }
     __syncthreads();
-    // Input rows k*N + 256*blk .. +255 are staged through an LDS tile of ETILE rows:
+    // Input rows k*N + EW*blk .. +EW-1 are staged through an LDS tile of ETILE rows:
     // each thread moves one 16-byte piece per tile (coalesced), loaded into
     // registers one tile ahead (the loads fly while the previous tile is coded).
     constexpr uint32_t ETILE = 16;
-    __shared__ __attribute__((aligned(16))) uint8_t itile[ETILE * 256];
-    const uint32_t s = blk * 256 + threadIdx.x;
+    __shared__ __attribute__((aligned(16))) uint8_t itile[ETILE * EW];
+    const uint32_t s = blk * EW + threadIdx.x;
     const bool active = s < N;
     const uint64_t c = active ? (n - s - 1) / N + 1 : 0;  // symbols s, s+N, ... < n
     const uint64_t cmax = (n - 1) / N + 1;
     const uint8_t *inb = raw + a.raw_off[b];
     const bool vec_in = ((((uintptr_t)inb) | N) & 15) == 0;
-    const uint32_t lr = threadIdx.x >> 4, lp = (threadIdx.x & 15) * 16;  // my piece: row, column
+    constexpr uint32_t PPR = EW / 16;  // 16-byte pieces per row (ETILE rows x PPR = EW pieces per tile)
+    const uint32_t lr = threadIdx.x / PPR, lp = (threadIdx.x % PPR) * 16;  // my piece: row, column
     auto load_piece = [&](uint64_t t) -> uint4 {
         const uint64_t k = t * ETILE + lr;
-        const uint64_t p = k * N + (uint64_t)blk * 256 + lp;
+        const uint64_t p = k * N + (uint64_t)blk * EW + lp;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < cmax && blk * 256 + lp < N) {
+        if (k < cmax && blk * EW + lp < N) {
             if (vec_in && p + 16 <= n) {
                 v = *reinterpret_cast<const uint4 *>(inb + p);
             } else {
                 uint32_t wv[4] = {0, 0, 0, 0};
                 for (uint32_t j = 0; j < 16; j++)
-                    if (p + j < n && blk * 256 + lp + j < N) wv[j >> 2] |= (uint32_t)inb[p + j] << (8 * (j & 3));
+                    if (p + j < n && blk * EW + lp + j < N) wv[j >> 2] |= (uint32_t)inb[p + j] << (8 * (j & 3));
                 v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
             }
         }
@@ -464,7 +482,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     // every 64 bytes a lane stores its 4 staged chunks back to back, so each
     // 64-B segment of the scratch reaches the L2 in one burst (16-B stores
     // spread over time were written back as partial lines: 2.4x the bytes).
-    __shared__ v4u stg[4 * 256];
+    __shared__ v4u stg[4 * EW];
     uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0, nstg = 0;
     v4u *out4 = reinterpret_cast<v4u *>(out);
     auto flush = [&]() {
@@ -480,7 +498,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         const bool need = nq == 4;
         if (__builtin_amdgcn_ballot_w64(need) != 0) {  // wave-uniform
             if (need) {
-                stg[(nstg & 3) * 256 + threadIdx.x] = v4u{q0, q1, q2, q3};
+                stg[(nstg & 3) * EW + threadIdx.x] = v4u{q0, q1, q2, q3};
                 nstg++;
                 nq = 0;
             }
@@ -489,13 +507,13 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
                 sc += 4;
                 if (full) {
                     const uint32_t o = nout >> 2;
-                    if (ablate & 1) {  // diagnostic
+                    if (ABL & 1) {  // diagnostic
                         asm volatile("" ::"v"(stg[threadIdx.x]));
                     } else {
-                        out4[o + 0] = stg[0 * 256 + threadIdx.x];
-                        out4[o + 1] = stg[1 * 256 + threadIdx.x];
-                        out4[o + 2] = stg[2 * 256 + threadIdx.x];
-                        out4[o + 3] = stg[3 * 256 + threadIdx.x];
+                        out4[o + 0] = stg[0 * EW + threadIdx.x];
+                        out4[o + 1] = stg[1 * EW + threadIdx.x];
+                        out4[o + 2] = stg[2 * EW + threadIdx.x];
+                        out4[o + 3] = stg[3 * EW + threadIdx.x];
                     }
                     nout += 16;
                 }
@@ -506,8 +524,8 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     // wait for the scratch stores); the wait counts this wave's stores since.
     auto issue_piece = [&](uint64_t t, v4u &dst) {
         const uint64_t k = t * ETILE + lr;
-        const uint64_t p = k * N + (uint64_t)blk * 256 + lp;
-        if (vec_in && k < cmax && blk * 256 + lp + 16 <= N && p + 16 <= n) {
+        const uint64_t p = k * N + (uint64_t)blk * EW + lp;
+        if (vec_in && k < cmax && blk * EW + lp + 16 <= N && p + 16 <= n) {
             asm_load16(dst, (uintptr_t)(inb + p));
         } else {
             const uint4 v = load_piece(t);
@@ -524,19 +542,19 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     for (uint64_t t = ntiles; t-- > 0;) {
         __syncthreads();
         wait_vmcnt_le(sc, pend);  // sc is wave-uniform
-        *reinterpret_cast<v4u *>(&itile[lr * 256 + lp]) = pend;
+        *reinterpret_cast<v4u *>(&itile[lr * EW + lp]) = pend;
         __syncthreads();
         sc = 0;
         if (t > 0) issue_piece(t - 1, pend);
         const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
-        const bool wave_all = (uint64_t)blk * 256 + (threadIdx.x & ~63u) + 64 <= N;  // wave-uniform
+        const bool wave_all = (uint64_t)blk * EW + (threadIdx.x & ~63u) + 64 <= N;  // wave-uniform
         if (rtop == ETILE && t * ETILE + ETILE < cmax && wave_all) {
             // full tile, every lane of the wave a stream: no per-lane predicates
 #pragma unroll
             for (int g = ETILE - 4; g >= 0; g -= 4) {
-                uint32_t s3 = itile[(g + 3) * 256 + threadIdx.x], s2 = itile[(g + 2) * 256 + threadIdx.x];
-                uint32_t s1 = itile[(g + 1) * 256 + threadIdx.x], s0 = itile[g * 256 + threadIdx.x];
-                if (ablate & 2) {  // diagnostic: conflict-free table reads (consecutive entries)
+                uint32_t s3 = itile[(g + 3) * EW + threadIdx.x], s2 = itile[(g + 2) * EW + threadIdx.x];
+                uint32_t s1 = itile[(g + 1) * EW + threadIdx.x], s0 = itile[g * EW + threadIdx.x];
+                if (ABL & 2) {  // diagnostic: conflict-free table reads (consecutive entries)
                     const uint32_t t = (threadIdx.x + (s0 & 1)) & 255;
                     s3 = s2 = s1 = s0 = t;
                 }
@@ -552,8 +570,8 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
             // full tile: every row is complete for every stream (rows < cmax - 1)
 #pragma unroll
             for (int g = ETILE - 4; g >= 0; g -= 4) {
-                const uint32_t s3 = itile[(g + 3) * 256 + threadIdx.x], s2 = itile[(g + 2) * 256 + threadIdx.x];
-                const uint32_t s1 = itile[(g + 1) * 256 + threadIdx.x], s0 = itile[g * 256 + threadIdx.x];
+                const uint32_t s3 = itile[(g + 3) * EW + threadIdx.x], s2 = itile[(g + 2) * EW + threadIdx.x];
+                const uint32_t s1 = itile[(g + 1) * EW + threadIdx.x], s0 = itile[g * EW + threadIdx.x];
                 const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
                 enc_step(e3, active);
                 enc_step(e2, active);
@@ -565,7 +583,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         } else {
             for (uint32_t r = rtop; r-- > 0;) {
                 const uint64_t k = t * ETILE + r;
-                const uint32_t sym = itile[r * 256 + threadIdx.x];
+                const uint32_t sym = itile[r * EW + threadIdx.x];
                 enc_step(et[sym], k < c);
                 flush();
             }
@@ -573,7 +591,7 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
     }
     wait_vmcnt_le(0, pend);
     // drain: staged chunks, queued dwords (oldest in q[4-nq]), the partial dword
-    for (uint32_t i = 0; i < (nstg & 3); i++) out4[(nout >> 2) + i] = stg[i * 256 + threadIdx.x];
+    for (uint32_t i = 0; i < (nstg & 3); i++) out4[(nout >> 2) + i] = stg[i * EW + threadIdx.x];
     nout += 4 * (nstg & 3);
     {
         const uint32_t qs[4] = {q0, q1, q2, q3};
@@ -588,8 +606,16 @@ __global__ __launch_bounds__(256) void k_enc_xn(const uint8_t *raw, KArgs a, Ran
         w.st_state[(size_t)b * N + s] = X >> 8;
         w.st_len[(size_t)b * N + s] = bytes;
     }
-    const uint64_t bs = block_sum(active ? bytes : 0, sh);
-    if (threadIdx.x == 0) w.blocksum[(size_t)b * nblk + blk] = bs;
+    // byte sum of the 256-stream block (the unit of the offset scan)
+    if (EW == 256) {
+        const uint64_t bs = block_sum(active ? bytes : 0, sh);
+        if (threadIdx.x == 0) w.blocksum[(size_t)b * w.nblk + blk] = bs;
+    } else {  // narrow workgroups add their wave sums into the zeroed block sum
+        const uint64_t ws = wave_sum(active ? bytes : 0);
+        if ((threadIdx.x & 63) == 0 && s < N)
+            atomicAdd(reinterpret_cast<unsigned long long *>(&w.blocksum[(size_t)b * w.nblk + s / 256]),
+                      (unsigned long long)ws);
+    }
 }
 
 // ======================================================================
@@ -656,6 +682,7 @@ __global__ __launch_bounds__(256) void k_scan(KArgs a, RansWork w, int decode) {
     }
 }
 
+#ifdef ZR_DIAG  // the previous compaction, kept for A/B runs (ZR_COMPACT_OLD=1)
 // header + stream compaction of the xN layout (rans.rs:402-419)
 constexpr uint32_t CSPLIT = 4;  // workgroups per 256-stream block (more bytes in flight per CU)
 __global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, RansWork w) {
@@ -764,6 +791,8 @@ __global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, Rans
         }
     }
 }
+
+#endif
 
 __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, RansWork w) {
     const uint32_t b = blockIdx.x;
@@ -1139,7 +1168,6 @@ __global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw
 //   * output: step k of stream s is raw[k*N + s]: per step one buffer byte
 //     store per wave, row offset in an SGPR, no VALU address work.
 // ----------------------------------------------------------------------
-constexpr int FW2 = 1024;
 constexpr int RR = 32;   // ring rows (dwords) per lane
 constexpr int DT2 = 16;  // steps per tile
 
@@ -1153,12 +1181,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(u), 0, 0x7FFFFFFF, 0x00020000);
 }
 
-// ABL: diagnostic ablations for profiling only (1: no output stores, 2: no slot
-// table read, 4: no ring refills, 8: per-workgroup timeline records written to
-// the workspace scratch area); the product path instantiates ABL = 0.
-template <int ABL>
-__global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
-                                                uint32_t nblkF) {
+// FW: workgroup width (1024 = one workgroup per CU sharing one table copy at
+// 2^18 streams; 64 = one wave per workgroup, which spreads a batch of few
+// streams, e.g. one buffer x 4096 streams, over that many CUs).
+// ABL: diagnostic ablations for profiling only, ZR_DIAG builds (1: no output
+// stores, 2: no slot table read, 4: no ring refills, 8: per-workgroup timeline
+// records written to the workspace scratch area); the product instantiates ABL = 0.
+template <int FW, int ABL>
+__global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
+                                               uint32_t nblkF) {
     const uint32_t b = blockIdx.x / nblkF, blkF = blockIdx.x % nblkF;
     const uint64_t dbg_t0 = (ABL & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t dbg_c0 = (ABL & 8) ? __builtin_amdgcn_s_memtime() : 0;
@@ -1166,7 +1197,7 @@ __global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
     if (n == 0 || single_mode(n, N) || a.status[b] != 0) return;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[TOTFREQ + (RR + 1) * FW2];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[TOTFREQ + (RR + 1) * FW];
     uint32_t *ring = lds + TOTFREQ;
     // scan scratch and flag alias the ring (used before it is filled)
     unsigned long long *sh = reinterpret_cast<unsigned long long *>(ring);
@@ -1176,10 +1207,10 @@ __global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t
     {
         const v4u *src = reinterpret_cast<const v4u *>(T->slot);
         v4u *dst = reinterpret_cast<v4u *>(lds);
-        dst[tid] = src[tid];
+        for (uint32_t j = tid; j < TOTFREQ / 4; j += FW) dst[j] = src[j];
     }
     const uint32_t kind = T->kind;
-    const uint32_t s = blkF * FW2 + tid;
+    const uint32_t s = blkF * FW + tid;
     const bool active = s < N;
     const uint8_t *e = enc + a.enc_off[b];
     const uint32_t L = active ? ld_u32_u(e + 8 * (size_t)N + 4 * (size_t)s) : 0;
@@ -1191,16 +1222,24 @@ __global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t
     unsigned long long base = 0;
     for (int i = 0; i < wv; i++) base += sh[i];
     const uint32_t nblk = w.nblk;
-    const uint64_t off = base + inc - L + w.blockoff[(size_t)b * nblk + 4 * blkF];
+    // offset: the 256-stream block's scanned offset, plus (FW < 256) the
+    // lengths of the block's streams below this workgroup
+    const uint32_t blk0 = (blkF * FW) / 256, below = (blkF * FW) % 256;
+    uint64_t sub = 0;
+    if (FW < 256 && below) {
+        uint64_t v = 0;
+        for (uint32_t i = tid; i < below; i += FW) v += ld_u32_u(e + 8 * (size_t)N + 4 * ((size_t)blk0 * 256 + i));
+        sub = wave_sum(v);  // FW < 256 is one wave
+    }
+    const uint64_t off = base + inc - L + w.blockoff[(size_t)b * nblk + blk0] + sub;
     const uint64_t X = active ? ld_u64_u(e + 8 * (size_t)s) : RANS_L;
     const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24);
     if (!fast) atomicOr(flag, 1u);
     __syncthreads();
     const uint32_t any_slow = *flag;
     __syncthreads();  // scan/flag reads complete before the ring is written
-    auto mark_redo = [&]() {
-        for (uint32_t i = 0; i < 4; i++)
-            if (4 * blkF + i < nblk) w.redo[(size_t)b * nblk + 4 * blkF + i] = 1;
+    auto mark_redo = [&]() {  // the 256-stream blocks this workgroup covers
+        for (uint32_t i = blk0; i <= (blkF * FW + FW - 1) / 256 && i < nblk; i++) w.redo[(size_t)b * nblk + i] = 1;
     };
     if (any_slow) {
         if (tid == 0) mark_redo();
@@ -1216,12 +1255,12 @@ __global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t
     // write the 64-B segment at absolute address g (64-aligned; cK = bytes g+16K..)
     auto put_seg = [&](uint32_t g, const v4u c0, const v4u c1, const v4u c2, const v4u c3) {
         const uint32_t r0 = ((g >> 2) + 1) & (RR - 1);  // 1 or 17
-        uint32_t *p = lring + r0 * FW2;
-        p[0 * FW2] = c0.x; p[1 * FW2] = c0.y; p[2 * FW2] = c0.z; p[3 * FW2] = c0.w;
-        p[4 * FW2] = c1.x; p[5 * FW2] = c1.y; p[6 * FW2] = c1.z; p[7 * FW2] = c1.w;
-        p[8 * FW2] = c2.x; p[9 * FW2] = c2.y; p[10 * FW2] = c2.z; p[11 * FW2] = c2.w;
-        p[12 * FW2] = c3.x; p[13 * FW2] = c3.y; p[14 * FW2] = c3.z;
-        p[15 * FW2] = c3.w;                      // row 16, or the mirror row 32
+        uint32_t *p = lring + r0 * FW;
+        p[0 * FW] = c0.x; p[1 * FW] = c0.y; p[2 * FW] = c0.z; p[3 * FW] = c0.w;
+        p[4 * FW] = c1.x; p[5 * FW] = c1.y; p[6 * FW] = c1.z; p[7 * FW] = c1.w;
+        p[8 * FW] = c2.x; p[9 * FW] = c2.y; p[10 * FW] = c2.z; p[11 * FW] = c2.w;
+        p[12 * FW] = c3.x; p[13 * FW] = c3.y; p[14 * FW] = c3.z;
+        p[15 * FW] = c3.w;                      // row 16, or the mirror row 32
         if (r0 != 1) lring[0] = c3.w;            // row 0 itself
     };
     // prologue: the 64-B segment holding the last stream byte and the one below
@@ -1241,8 +1280,8 @@ __global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t
     uint32_t x = (uint32_t)X;
     // D: the 4 stream bytes below p (byte p-1 on top)
     auto readD = [&](uint32_t p8) -> uint32_t {
-        const uint32_t *q = lring + ((p8 >> 5) & (RR - 1)) * FW2;
-        return __builtin_amdgcn_alignbit(q[FW2], q[0], p8);
+        const uint32_t *q = lring + ((p8 >> 5) & (RR - 1)) * FW;
+        return __builtin_amdgcn_alignbit(q[FW], q[0], p8);
     };
     // one decode step (rans.rs:472-507): renormalise from window D, decode, return
     // the slot entry; hi/lo are the shifted (x : D) pair, sft = 8 + 8 * bytes consumed
@@ -1263,10 +1302,10 @@ __global__ __launch_bounds__(FW2) void k_dec_xn_fast(const uint8_t *enc, uint8_t
     bool pnd = false;  // this lane has a segment in flight
     uint32_t ptile = 0;
     bool bad = false;
-    const uint64_t wbase = (uint64_t)blkF * FW2 + (tid & ~63u);
+    const uint64_t wbase = (uint64_t)blkF * FW + (tid & ~63u);
     const bool wave_live = wbase < N;       // wave-uniform
     const bool wave_all = wbase + 64 <= N;  // wave-uniform
-    uint8_t *outb = raw + a.raw_off[b] + (size_t)blkF * FW2;
+    uint8_t *outb = raw + a.raw_off[b] + (size_t)blkF * FW;
     // output rows are addressed through a descriptor rebased every tile, so the
     // 32-bit buffer offsets cover any buffer size
     __amdgpu_buffer_rsrc_t orsrc = byte_rsrc(outb);
@@ -1724,6 +1763,34 @@ __global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t
 
 
 // ======================================================================
+// exhaustive check of the encoder's reciprocal division (the analogue of the
+// reference's fast_div test, rans.rs:786-809): for every freq in 1..4096 and
+// every x < 2^24 (the encoder only divides x < freq << 12 after
+// renormalisation), enc_div(x) must equal x / freq. A workgroup takes one
+// freq and 2^18 consecutive x; each thread walks 1024 x keeping the true
+// quotient incrementally (one hardware division per thread).
+// ======================================================================
+__global__ __launch_bounds__(256) void k_rcp_selftest(unsigned long long *bad, uint32_t *first) {
+    const uint32_t f = blockIdx.x / 64 + 1;
+    const uint32_t x0 = (blockIdx.x % 64) * (1u << 18) + threadIdx.x * 1024;
+    const uint32_t rcp = enc_rcp(f), rsh = enc_rsh(f);
+    uint32_t q = x0 / f, r = x0 % f;
+    uint32_t nbad = 0;
+    for (uint32_t i = 0; i < 1024; i++) {
+        const uint32_t x = x0 + i;
+        if (enc_div(x, rcp, rsh) != q) {
+            if (nbad == 0) atomicCAS(first, 0u, f);  // a failing freq, for diagnosis
+            nbad++;
+        }
+        if (++r == f) {
+            r = 0;
+            q++;
+        }
+    }
+    if (nbad) atomicAdd(bad, (unsigned long long)nbad);
+}
+
+// ======================================================================
 // host launchers
 // ======================================================================
 // per-stream scratch stride: a multiple of 128 B, so the encoder's 64-byte
@@ -1771,6 +1838,13 @@ int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t by
     return ZR_OK;
 }
 
+// Few streams in the whole batch (e.g. one 256 MiB buffer x 4096 streams,
+// BASELINE configs[1] as written): one wave per workgroup, so the lanes spread
+// over as many CUs as there are waves (up to 1024 workgroups: 4 per CU, each
+// with its own 16 KiB table copy, fit the LDS) instead of a few 1024-lane or
+// 256-lane workgroups on a handful of CUs.
+static bool narrow_batch(const KArgs &a) { return (uint64_t)a.B * a.N <= (1u << 16); }
+
 static KArgs kargs(const zr_rans_batch *bt) {
     KArgs a;
     a.B = bt->n_buffers;
@@ -1793,6 +1867,28 @@ using namespace zr;
 extern "C" {
 
 size_t zr_rans_dtab_bytes(void) { return sizeof(RansDTab); }
+
+int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!mismatches) return set_error(ZR_INVALID_INPUT, "null argument");
+    CallLease L;
+    int32_t st = L.acquire();
+    if (st) return st;
+    void *d;
+    if ((st = L.get(2, 64, &d))) return st;
+    hipStream_t s = L.stream();
+    ZR_HIP(hipMemsetAsync(d, 0, 64, s));
+    hipLaunchKernelGGL(k_rcp_selftest, dim3(4096 * 64), dim3(256), 0, s, reinterpret_cast<unsigned long long *>(d),
+                       reinterpret_cast<uint32_t *>(d) + 4);
+    ZR_HIP(hipGetLastError());
+    uint64_t *meta = L.ctx()->meta;
+    ZR_HIP(hipMemcpyAsync(meta, d, 8, hipMemcpyDeviceToHost, s));
+    if ((st = L.sync())) return st;
+    *mismatches = meta[0];
+    return ZR_OK;
+    ZR_GUARD_END
+}
 
 size_t zr_rans_workspace_bytes(uint32_t n_buffers, uint32_t n_streams, uint64_t max_len) {
     return rans_workspace_bytes(n_buffers, n_streams, max_len);
@@ -1842,6 +1938,8 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
     clear_error();
     if (!bt) return set_error(ZR_INVALID_INPUT, "null batch");
     if (bt->n_buffers == 0) return ZR_OK;
+    if (bt->n_streams >= (1u << 27))  // the decoder's limit: refuse what could not be decoded
+        return set_error(ZR_UNSUPPORTED, "more than 2^27 rANS streams");
     KArgs a = kargs(bt);
     RansWork w;
     int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
@@ -1850,19 +1948,33 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
     ZR_HIP(hipMemsetAsync(bt->status, 0, sizeof(int32_t) * a.B, s));
     const uint64_t gx = (uint64_t)w.nblk * a.B;
     if (bt->max_len >= a.N && a.N > 1) {
+        const bool narrow = narrow_batch(a);
+        if (narrow)  // the narrow encoder adds wave sums into the block sums
+            ZR_HIP(hipMemsetAsync(w.blocksum, 0, sizeof(uint64_t) * gx, s));
         timer_begin("rans_encode", s);
-        static const int ablate = getenv("ZR_ABLATE") ? atoi(getenv("ZR_ABLATE")) : 0;  // diagnostics only
-        hipLaunchKernelGGL(k_enc_xn, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w, ablate);
+#ifdef ZR_DIAG
+        static const int ablate = getenv("ZR_ABLATE") ? atoi(getenv("ZR_ABLATE")) : 0;
+        auto kenc = ablate == 1 ? k_enc_xn<256, 1> : ablate == 2 ? k_enc_xn<256, 2> : ablate == 3 ? k_enc_xn<256, 3>
+                                                                                            : k_enc_xn<256, 0>;
+#else
+        auto kenc = k_enc_xn<256, 0>;
+#endif
+        if (narrow)
+            hipLaunchKernelGGL((k_enc_xn<64, 0>), dim3((uint32_t)(ceil_div(a.N, 64) * a.B)), dim3(64), 0, s, raw, a, w);
+        else
+            hipLaunchKernelGGL(kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
         timer_end("rans_encode", s);
-        static const int cmp_old = getenv("ZR_COMPACT_OLD") ? 1 : 0;  // A/B diagnostics
-        if (cmp_old) hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
         timer_begin("rans_compact", s);
-        if (cmp_old)
+#ifdef ZR_DIAG
+        static const int cmp_old = getenv("ZR_COMPACT_OLD") ? 1 : 0;  // A/B diagnostics
+        if (cmp_old) {
+            hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
             hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
-        else  // 16 streams per workgroup, 19 KiB window (8 workgroups per CU), four 16-B loads in
-              // flight per lane (A/B: 0.140 -> 0.132 ms over two); block-sum scan fused in
-            hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 4>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc,
-                               a, w);
+        } else
+#endif
+        // 16 streams per workgroup, 19 KiB window (8 workgroups per CU), four 16-B loads in
+        // flight per lane (A/B: 0.140 -> 0.132 ms over two); block-sum scan fused in
+        hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 4>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
         timer_end("rans_compact", s);
     }
     timer_begin("rans_encode_x1", s);
@@ -1886,6 +1998,8 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
     clear_error();
     if (!bt) return set_error(ZR_INVALID_INPUT, "null batch");
     if (bt->n_buffers == 0) return ZR_OK;
+    if (bt->n_streams >= (1u << 27))  // a tile of DT2 output rows must span < 2^31 bytes
+        return set_error(ZR_UNSUPPORTED, "more than 2^27 rANS streams");
     KArgs a = kargs(bt);
     RansWork w;
     int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
@@ -1897,20 +2011,27 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
         hipLaunchKernelGGL(k_dec_hdr, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
         hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
         timer_begin("rans_decode", s);
-        if (a.N >= (1u << 27))  // a tile of DT2 output rows must span < 2^31 bytes
-            return set_error(ZR_UNSUPPORTED, "more than 2^27 rANS streams");
-        const uint32_t nblkF = (uint32_t)ceil_div(a.N, FW2);
-        static const int abl = getenv("ZR_DEC_ABL") ? atoi(getenv("ZR_DEC_ABL")) : 0;  // profiling only
-        auto kern = k_dec_xn_fast<0>;
-        switch (abl) {
-            case 1: kern = k_dec_xn_fast<1>; break;
-            case 2: kern = k_dec_xn_fast<2>; break;
-            case 4: kern = k_dec_xn_fast<4>; break;
-            case 7: kern = k_dec_xn_fast<7>; break;
-            case 8: kern = k_dec_xn_fast<8>; break;
-            default: break;
+        if (narrow_batch(a)) {
+            const uint32_t nblkF = (uint32_t)ceil_div(a.N, 64);
+            hipLaunchKernelGGL((k_dec_xn_fast<64, 0>), dim3(nblkF * a.B), dim3(64), 0, s, enc, raw, a, w, nblkF);
+        } else {
+            const uint32_t nblkF = (uint32_t)ceil_div(a.N, 1024);
+#ifdef ZR_DIAG
+            static const int abl = getenv("ZR_DEC_ABL") ? atoi(getenv("ZR_DEC_ABL")) : 0;  // profiling only
+            auto kern = k_dec_xn_fast<1024, 0>;
+            switch (abl) {
+                case 1: kern = k_dec_xn_fast<1024, 1>; break;
+                case 2: kern = k_dec_xn_fast<1024, 2>; break;
+                case 4: kern = k_dec_xn_fast<1024, 4>; break;
+                case 7: kern = k_dec_xn_fast<1024, 7>; break;
+                case 8: kern = k_dec_xn_fast<1024, 8>; break;
+                default: break;
+            }
+#else
+            auto kern = k_dec_xn_fast<1024, 0>;
+#endif
+            hipLaunchKernelGGL(kern, dim3(nblkF * a.B), dim3(1024), 0, s, enc, raw, a, w, nblkF);
         }
-        hipLaunchKernelGGL(kern, dim3(nblkF * a.B), dim3(FW2), 0, s, enc, raw, a, w, nblkF);
         timer_end("rans_decode", s);
         hipLaunchKernelGGL(k_dec_xn<true>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
     }

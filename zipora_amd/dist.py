@@ -16,8 +16,17 @@ def world():
 
 
 def allreduce_histogram(hist):
-    """Sum a 256-bin histogram (uint32 or int64 tensor, any device) over ranks in place."""
+    """Sum a 256-bin histogram (int32/uint32 or int64 tensor, any device) over ranks in place.
+
+    int32 counts are the device histograms' u32 bit patterns: the sum wraps mod
+    2^32 exactly as the reference's u32 counts do. RCCL reduces device tensors
+    in place; gloo (CPU tests) reduces a host copy of a device tensor."""
     if world() == 1:
+        return hist
+    if hist.is_cuda and dist.get_backend() == "gloo":
+        h = hist.cpu()
+        allreduce_histogram(h)
+        hist.copy_(h)
         return hist
     if hist.dtype == torch.int32 or hist.dtype == torch.int64:
         dist.all_reduce(hist, op=dist.ReduceOp.SUM)

@@ -88,6 +88,51 @@ class Rans64Decoder:
         return ctypes.string_at(out, output_length)
 
 
+class AdaptiveRans64Encoder:
+    """AdaptiveRans64Encoder (rans.rs:655-721): picks P by the data size."""
+
+    _NAMES = {1: "x1", 2: "x2", 4: "x4", 8: "x8"}
+    _VARIANTS = {1: ParallelX1, 2: ParallelX2, 4: ParallelX4, 8: ParallelX8}
+
+    def __init__(self):
+        pass
+
+    @classmethod
+    def new(cls):
+        return cls()
+
+    def select_variant(self, data_size):
+        """select_variant (rans.rs:669-681): "x1" < 73 <= "x2" < 73^2 <= "x4" < 73^4 <= "x8"."""
+        return self._NAMES[_lib.load().zr_rans_adaptive_streams(int(data_size))]
+
+    def variant_for(self, data_size):
+        return self._VARIANTS[_lib.load().zr_rans_adaptive_streams(int(data_size))]
+
+    def encode_adaptive(self, data):
+        """encode_adaptive (rans.rs:684-706): histogram + Rans64Encoder::<P>::new + encode."""
+        L = _lib.load()
+        buf, n = _u8(data)
+        cap = L.zr_rans_encode_bound(n, 8)
+        out = (ctypes.c_uint8 * cap)()
+        ol = ctypes.c_size_t(0)
+        used = ctypes.c_uint32(0)
+        check(L.zr_rans_encode_adaptive(buf, n, out, cap, ctypes.byref(ol), ctypes.byref(used)))
+        return ctypes.string_at(out, ol.value)
+
+
+def selftest_reciprocal():
+    """Mismatches of the device encoder division over every freq 1..4096 and x < 2^24."""
+    v = ctypes.c_uint64(0)
+    check(_lib.load().zr_rans_selftest_reciprocal(ctypes.byref(v)))
+    return v.value
+
+
+def device_alloc_count():
+    v = ctypes.c_uint64(0)
+    check(_lib.load().zr_device_alloc_count(ctypes.byref(v)))
+    return v.value
+
+
 def histogram(data):
     import numpy as np
     d = np.frombuffer(bytes(data), dtype=np.uint8)
@@ -95,4 +140,5 @@ def histogram(data):
 
 
 __all__ = ["ParallelVariant", "ParallelX1", "ParallelX2", "ParallelX4", "ParallelX8",
-           "Rans64Encoder", "Rans64Decoder", "Rans64Symbol", "ZiporaError", "histogram"]
+           "Rans64Encoder", "Rans64Decoder", "Rans64Symbol", "AdaptiveRans64Encoder", "ZiporaError", "histogram",
+           "selftest_reciprocal", "device_alloc_count"]
