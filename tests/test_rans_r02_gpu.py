@@ -127,13 +127,12 @@ def test_device_table_wrapped_total(zr, oracle):
     h = [0] * 256
     h[0], h[255] = 0x80000000, 0x80000001  # total wraps to 1
     hists.append(h)
-    for _ in range(30):
+    while len(hists) < 32:
         h = [rnd.choice([0, 0, 1, rnd.randrange(1, 1000)]) for _ in range(256)]
         for _ in range(rnd.randrange(1, 4)):
             h[rnd.randrange(256)] = rnd.randrange(1 << 30, 1 << 32)
-        if sum(h) & 0xFFFFFFFF == 0:
-            h[3] += 1
-        hists.append(h)
+        if sum(h) >= (1 << 32) and sum(h) & 0xFFFFFFFF:
+            hists.append(h)
     assert all(sum(h) >= (1 << 32) for h in hists)
     bt = RansDeviceBatch([1] * len(hists), 1, shared_table=False)
     bt.hist.copy_(torch.tensor(np.array(hists, dtype=np.uint32).view(np.int32).reshape(-1)).cuda())

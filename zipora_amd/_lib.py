@@ -9,10 +9,10 @@ import os
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libzipora_amd.so")
 # tools only: ZR_DIAG_LIB=1 loads the -DZR_DIAG build (profiling ablations that
-# read ZR_ABLATE / ZR_DEC_ABL / ZR_COMPACT_OLD); bench.py refuses to print a
-# metric line from it
+# read ZR_ABLATE / ZR_DEC_ABL / ZR_COMPACT_OLD), ZR_LIB_PATH another build (A/B
+# runs); bench.py refuses to print a metric line under either
 DIAG_LIB_PATH = os.path.join(_PKG, "libzipora_amd_diag.so")
-DIAG_ENV = ("ZR_DIAG_LIB", "ZR_ABLATE", "ZR_DEC_ABL", "ZR_COMPACT_OLD")
+DIAG_ENV = ("ZR_DIAG_LIB", "ZR_LIB_PATH", "ZR_ABLATE", "ZR_DEC_ABL", "ZR_COMPACT_OLD")
 
 
 def diag_env():
@@ -195,6 +195,8 @@ def load(build_if_missing=True):
         pass
     diag = bool(os.environ.get("ZR_DIAG_LIB"))
     path = DIAG_LIB_PATH if diag else LIB_PATH
+    if os.environ.get("ZR_LIB_PATH"):  # tools only (A/B of two builds on one box)
+        path = os.environ["ZR_LIB_PATH"]
     if not os.path.exists(path):
         if not build_if_missing:
             raise RuntimeError(f"zipora_amd: HIP library missing at {path}; run "

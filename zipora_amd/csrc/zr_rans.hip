@@ -403,7 +403,6 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // 0xFFFF = never, freq >= 16); y = start << 8; z = reciprocal;
     // w = (4096 - freq) << 8 | rsh << 24 (mad_u24 reads the low 24 bits)
     __shared__ uint4 et[256];
-    __shared__ unsigned long long sh[4];
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
     for (uint32_t v = threadIdx.x; v < 256; v += EW) {
         const uint32_t f = T->freq[v];
@@ -442,9 +441,9 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         return v;
     };
     uint32_t *out = reinterpret_cast<uint32_t *>(w.scratch + (size_t)b * w.region + (size_t)s * w.cap);
-    uint32_t X = RANS_L << 8, nout = 0;  // nout = dwords stored
+    uint32_t X = RANS_L << 8;
     uint64_t acc = 0;               // pending output bits (emission order from bit 0)
-    uint32_t nacc = 0;              // valid bits in acc, < 32 after every flush
+    uint32_t nacc = 0;              // valid bits in acc, < 32 after every push
     bool err = false;
     // encode_symbol (rans.rs:303-335), branchless: at most two renorm bytes
     // (x < 2^24, xmax >= 2^12); q = x / f by the exact 24-bit reciprocal.
@@ -477,46 +476,38 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         X = valid ? xn : X;
     };
     uint32_t sc = 0;  // store instructions this wave issued since the last piece load
-    // full dwords queue in a 4-dword shift register; every 16 bytes move to an
-    // LDS staging row ([chunk][lane], 1 KiB per wave store: conflict-free), and
-    // every 64 bytes a lane stores its 4 staged chunks back to back, so each
-    // 64-B segment of the scratch reaches the L2 in one burst (16-B stores
-    // spread over time were written back as partial lines: 2.4x the bytes).
-    __shared__ v4u stg[4 * EW];
-    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, nq = 0, nstg = 0;
+    // Output: after every pair of steps the low dword of acc is written to a
+    // per-lane LDS ring ([slot][lane]: conflict-free) at slot nw, and nw
+    // advances only when that dword is complete (nacc >= 32): no branch, no
+    // register queue. At each tile boundary a lane with 16 complete dwords
+    // (64 B) pending moves them to its scratch slot in one burst of four
+    // 16-B stores, so each 64-B half of a scratch line reaches the L2 whole.
+    // A tile adds at most 8 dwords, so at most 15 + 8 are pending: 32 slots.
+    constexpr uint32_t ERS = 32;
+    __shared__ uint32_t ring[ERS * EW];
+    uint32_t nw = 0, nfl = 0;  // dwords completed / moved to scratch
     v4u *out4 = reinterpret_cast<v4u *>(out);
-    auto flush = [&]() {
-        if (nacc >= 32) {
-            q0 = q1;
-            q1 = q2;
-            q2 = q3;
-            q3 = (uint32_t)acc;
-            acc >>= 32;
-            nacc -= 32;
-            nq++;
-        }
-        const bool need = nq == 4;
+    auto push = [&]() {
+        ring[(nw & (ERS - 1)) * EW + threadIdx.x] = (uint32_t)acc;
+        nw += nacc >> 5;  // nacc < 64 here
+        acc >>= (nacc & 32);
+        nacc &= 31;
+    };
+    auto flush64 = [&]() {  // tile boundary: at most one 64-B burst per lane
+        const bool need = nw - nfl >= 16;
         if (__builtin_amdgcn_ballot_w64(need) != 0) {  // wave-uniform
+            sc += 4;
             if (need) {
-                stg[(nstg & 3) * EW + threadIdx.x] = v4u{q0, q1, q2, q3};
-                nstg++;
-                nq = 0;
-            }
-            const bool full = need && (nstg & 3) == 0;
-            if (__builtin_amdgcn_ballot_w64(full) != 0) {
-                sc += 4;
-                if (full) {
-                    const uint32_t o = nout >> 2;
-                    if (ABL & 1) {  // diagnostic
-                        asm volatile("" ::"v"(stg[threadIdx.x]));
-                    } else {
-                        out4[o + 0] = stg[0 * EW + threadIdx.x];
-                        out4[o + 1] = stg[1 * EW + threadIdx.x];
-                        out4[o + 2] = stg[2 * EW + threadIdx.x];
-                        out4[o + 3] = stg[3 * EW + threadIdx.x];
-                    }
-                    nout += 16;
-                }
+                const uint32_t *r = ring + threadIdx.x;
+                uint32_t d[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) d[i] = r[((nfl + i) & (ERS - 1)) * EW];
+                const uint32_t o = nfl >> 2;
+                out4[o + 0] = v4u{d[0], d[1], d[2], d[3]};
+                out4[o + 1] = v4u{d[4], d[5], d[6], d[7]};
+                out4[o + 2] = v4u{d[8], d[9], d[10], d[11]};
+                out4[o + 3] = v4u{d[12], d[13], d[14], d[15]};
+                nfl += 16;
             }
         }
     };
@@ -546,6 +537,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         __syncthreads();
         sc = 0;
         if (t > 0) issue_piece(t - 1, pend);
+        if (!(ABL & 1)) flush64();
         const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
         const bool wave_all = (uint64_t)blk * EW + (threadIdx.x & ~63u) + 64 <= N;  // wave-uniform
         if (rtop == ETILE && t * ETILE + ETILE < cmax && wave_all) {
@@ -561,10 +553,10 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
                 const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
                 enc_fast(e3);
                 enc_fast(e2);
-                flush();
+                push();
                 enc_fast(e1);
                 enc_fast(e0);
-                flush();
+                push();
             }
         } else if (rtop == ETILE && t * ETILE + ETILE < cmax) {
             // full tile: every row is complete for every stream (rows < cmax - 1)
@@ -575,29 +567,33 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
                 const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
                 enc_step(e3, active);
                 enc_step(e2, active);
-                flush();
+                push();
                 enc_step(e1, active);
                 enc_step(e0, active);
-                flush();
+                push();
             }
         } else {
             for (uint32_t r = rtop; r-- > 0;) {
                 const uint64_t k = t * ETILE + r;
                 const uint32_t sym = itile[r * EW + threadIdx.x];
                 enc_step(et[sym], k < c);
-                flush();
+                push();
             }
         }
     }
     wait_vmcnt_le(0, pend);
-    // drain: staged chunks, queued dwords (oldest in q[4-nq]), the partial dword
-    for (uint32_t i = 0; i < (nstg & 3); i++) out4[(nout >> 2) + i] = stg[i * EW + threadIdx.x];
-    nout += 4 * (nstg & 3);
+    // drain: the pending complete dwords (16-B pieces, then single dwords), then
+    // the partial dword (its nacc / 8 whole bytes count)
     {
-        const uint32_t qs[4] = {q0, q1, q2, q3};
-        for (uint32_t i = 0; i < nq; i++) out[nout + i] = qs[4 - nq + i];
-        nout += nq;
+        const uint32_t *r = ring + threadIdx.x;
+        while (nw - nfl >= 4) {
+            out4[nfl >> 2] = v4u{r[(nfl & (ERS - 1)) * EW], r[((nfl + 1) & (ERS - 1)) * EW],
+                                 r[((nfl + 2) & (ERS - 1)) * EW], r[((nfl + 3) & (ERS - 1)) * EW]};
+            nfl += 4;
+        }
+        for (; nfl < nw; nfl++) out[nfl] = r[(nfl & (ERS - 1)) * EW];
     }
+    const uint32_t nout = nw;
     if (nacc) out[nout] = (uint32_t)acc;
     const uint32_t nacc_bytes = nacc / 8;
     if (err || xmin == 0) atomicOr(&a.status[b], 1);  // marked; converted to ZR_INVALID_INPUT by the scan
@@ -606,8 +602,12 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         w.st_state[(size_t)b * N + s] = X >> 8;
         w.st_len[(size_t)b * N + s] = bytes;
     }
-    // byte sum of the 256-stream block (the unit of the offset scan)
+    // byte sum of the 256-stream block (the unit of the offset scan); the
+    // scan scratch aliases the input tile, free once every wave is past it
+    // (the LDS budget is exactly four 40 KiB workgroups per CU)
     if (EW == 256) {
+        __syncthreads();
+        unsigned long long *sh = reinterpret_cast<unsigned long long *>(itile);
         const uint64_t bs = block_sum(active ? bytes : 0, sh);
         if (threadIdx.x == 0) w.blocksum[(size_t)b * w.nblk + blk] = bs;
     } else {  // narrow workgroups add their wave sums into the zeroed block sum
@@ -811,19 +811,26 @@ __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, Ra
 
 
 // Stream compaction through an LDS image of the destination (rans.rs:402-419):
-// a workgroup owns CS consecutive streams, whose bytes are contiguous in the
-// destination. Phase 1 reads each stream's scratch bytes with aligned 16-B
-// loads (a wave walks the flattened chunk list of its streams, CU_LD loads in
-// flight per lane) and writes them at their destination offsets into an LDS
-// window; phase 2 writes the window out with aligned 16-B stores. Only the
-// two edge units of the group, shared with the neighbouring groups, are
-// stored byte by byte. Windows repeat when a group's bytes exceed CWIN.
-template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD>  // streams per workgroup (divides 256), LDS window bytes, loads in flight per lane
-__global__ __launch_bounds__(256) void k_enc_compact_lds(uint8_t *enc, KArgs a, RansWork w) {
+// the CS consecutive streams of a group are contiguous in the destination.
+// Their destination span is cut into windows of CWIN bytes; workgroup
+// (group, w) builds windows w, w + nwin, w + 2 nwin, ... (nwin workgroups per
+// group, from the launch: one for short streams, many for the 64 KiB streams
+// of one 256 MiB buffer x 4096). Per window: phase 1 reads the 16-byte scratch
+// chunks that land in the window (CU_LD aligned 16-B loads in flight per lane)
+// and writes them at their destination offsets into the LDS image; phase 2
+// writes the image out with aligned 16-B stores. Only the two edge units of a
+// group, shared with the neighbouring groups, are stored byte by byte.
+// (8 waves per SIMD: 8 workgroups of 19 KiB LDS per CU, at most 64 VGPRs)
+template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD>  // streams per group (divides 64), window bytes, loads in flight
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_lds(
+    uint8_t *enc, KArgs a, RansWork w, uint32_t nwin) {
+    static_assert(CS <= 64 && 64 % CS == 0, "a group's streams are lanes of one wave");
     const uint32_t nblk = w.nblk;
     const uint32_t gpb = 256 / CS;  // groups per 256-stream block
     const uint32_t ngrp = nblk * gpb;
-    const uint32_t b = blockIdx.x / ngrp, grp = blockIdx.x % ngrp;
+    const uint32_t wi = blockIdx.x % nwin;
+    const uint32_t gid = blockIdx.x / nwin;
+    const uint32_t b = gid / ngrp, grp = gid % ngrp;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
@@ -833,78 +840,117 @@ __global__ __launch_bounds__(256) void k_enc_compact_lds(uint8_t *enc, KArgs a, 
     const uint32_t ns = min(CS, N - s0);
     __shared__ unsigned long long sh[4];
     __shared__ uint64_t soff[CS];
-    __shared__ uint32_t slen[CS], cpre[CS + 1];
+    __shared__ uint32_t slen[CS], cpre[CS + 1], clo[CS];
     __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
-    const uint32_t tid = threadIdx.x;
     // the buffer's scan of block byte sums (k_scan, fused): this block's
     // offset, and for group 0 the encoded length and the final status
     uint64_t below = 0, all = 0;
-    for (uint32_t i = tid; i < nblk; i += 256) {
+    for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
         const uint64_t v = w.blocksum[(size_t)b * nblk + i];
         below += i < blk ? v : 0;
         all += v;
     }
     const uint64_t bo = block_sum(below, sh);
-    if (grp == 0) {  // workgroup-uniform
+    if (grp == 0 && wi == 0) {  // workgroup-uniform
         const uint64_t tot = block_sum(all, sh);
-        if (tid == 0) {
+        if (threadIdx.x == 0) {
             a.enc_len[b] = (uint64_t)N * 12 + tot;
             if (a.status[b] != 0) a.status[b] = ZR_INVALID_INPUT;
         }
     }
     if (a.status[b] != 0) return;  // nonzero for every reader once marked by k_enc_xn
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    uint8_t *dbase = enc + a.enc_off[b] + 12 * (size_t)N;
+    // the chunks of stream i that land in the window [win, wend) of the image
+    // (image offset 0 = ua0, the group's first byte rounded down to 16):
+    // chunk c starts at image offset D_i + 16 c
+    auto chunk_range = [&](uint64_t soffi, uint32_t leni, uintptr_t ua0, uint64_t win, uint64_t wend,
+                           uint32_t &c0, uint32_t &cnt) {
+        const int64_t Di = (int64_t)((uintptr_t)dbase + soffi - ua0);
+        const int64_t nch = (leni + 15) >> 4;
+        const int64_t a0 = (int64_t)win - Di, a1 = (int64_t)wend - Di;  // window relative to the stream
+        const int64_t cl = a0 > 0 ? (a0 >> 4) : 0;
+        const int64_t ch = a1 > 0 ? min(nch, (a1 + 15) >> 4) : 0;
+        c0 = (uint32_t)cl;
+        cnt = ch > cl ? (uint32_t)(ch - cl) : 0u;
+    };
+    auto publish = [&](bool mine, uint32_t i, uint32_t c0, uint32_t cnt) {  // one wave: prefix of counts
+        uint32_t inc = cnt;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += t;
+        }
+        if (mine) {
+            cpre[i + 1] = inc;
+            clo[i] = c0;
+            if (i == 0) cpre[0] = 0;
+        }
+    };
+    uint64_t span = 0;
+    uintptr_t ua0 = 0;
     {
-        // offsets of the block's streams (block scan), keep this group's
+        // offsets of the block's streams (block scan), keep this group's; the
+        // group's first window workgroup writes their states and lengths. The
+        // group's streams are lanes [l0, l0 + ns) of one wave: the group's
+        // extent comes from its first and last lane, and the chunk ranges of
+        // the workgroup's first window are prefixed right here
         const uint32_t sb = blk * 256 + tid;
         const uint32_t i = sb - s0;
         const bool mine = sb >= s0 && i < ns;
         const uint32_t L = sb < N ? w.st_len[(size_t)b * N + sb] : 0;
-        const uint32_t X = mine ? w.st_state[(size_t)b * N + sb] : 0;
         const uint64_t off = block_excl_scan(L, sh, nullptr) + bo;
+        const uint32_t l0 = (s0 - blk * 256) & 63;
+        const uint64_t g_r0 = __shfl(off, (int)l0, 64);
+        const uint64_t g_r1 = __shfl(off + L, (int)(l0 + ns - 1), 64);
+        const uintptr_t g_ua0 = ((uintptr_t)dbase + g_r0) & ~(uintptr_t)15;
+        const uint64_t g_span = (uintptr_t)dbase + g_r1 - g_ua0;
         if (mine) {
             soff[i] = off;
             slen[i] = L;
-            uint8_t *e = enc + a.enc_off[b];
-            if ((((uintptr_t)e) & 7) == 0) {
-                *reinterpret_cast<uint2 *>(e + 8 * (size_t)sb) = make_uint2(X, 0);
-                *reinterpret_cast<uint32_t *>(e + 8 * (size_t)N + 4 * (size_t)sb) = L;
-            } else {
-                st_u32_u(e + 8 * (size_t)sb, X);
-                st_u32_u(e + 8 * (size_t)sb + 4, 0);
-                st_u32_u(e + 8 * (size_t)N + 4 * (size_t)sb, L);
+            if (wi == 0) {
+                const uint32_t X = w.st_state[(size_t)b * N + sb];
+                uint8_t *e = enc + a.enc_off[b];
+                if ((((uintptr_t)e) & 7) == 0) {
+                    *reinterpret_cast<uint2 *>(e + 8 * (size_t)sb) = make_uint2(X, 0);
+                    *reinterpret_cast<uint32_t *>(e + 8 * (size_t)N + 4 * (size_t)sb) = L;
+                } else {
+                    st_u32_u(e + 8 * (size_t)sb, X);
+                    st_u32_u(e + 8 * (size_t)sb + 4, 0);
+                    st_u32_u(e + 8 * (size_t)N + 4 * (size_t)sb, L);
+                }
             }
         }
-        // chunk-count prefix (16-B source chunks per stream): the group's
-        // streams are lanes i of the waves holding them; CS <= 64 and groups
-        // are aligned, so one wave holds them all
-        const uint32_t cc = mine ? (L + 15) >> 4 : 0;
-        uint32_t inc = cc;
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t t = __shfl_up(inc, d, 64);
-            if ((tid & 63) >= d) inc += t;
-        }
-        // the wave's lanes below the group contribute 0 only if the group
-        // starts at lane 0 of the wave or lanes below are not mine (true: cc = 0)
-        if (mine) cpre[i + 1] = inc;
-        if (mine && i == 0) cpre[0] = 0;
+        uint32_t c0 = 0, cnt = 0;
+        const uint64_t win0 = (uint64_t)wi * CWIN;
+        if (mine && g_r1 > g_r0) chunk_range(off, L, g_ua0, win0, min(g_span, win0 + (uint64_t)CWIN), c0, cnt);
+        if (wv == (s0 - blk * 256) / 64) publish(mine, i, c0, cnt);  // the group's wave (uniform branch)
     }
     __syncthreads();
-    uint8_t *dbase = enc + a.enc_off[b] + 12 * (size_t)N;
     const uint64_t r0 = soff[0], r1 = soff[ns - 1] + slen[ns - 1];
     if (r1 <= r0) return;
-    const uintptr_t ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
-    const uint64_t span = (uintptr_t)dbase + r1 - ua0;  // bytes of the image from ua0
-    const uint32_t nchunks = cpre[ns];
+    ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
+    span = (uintptr_t)dbase + r1 - ua0;  // bytes of the image from ua0
     const uint8_t *sbase = w.scratch + (size_t)b * w.region + (size_t)s0 * w.cap;
-    const uint32_t lane = tid & 63, wv = tid >> 6;
-    for (uint64_t win = 0; win < span; win += CWIN) {
+    const uint64_t lo = (uintptr_t)dbase + r0 - ua0;  // image bytes below lo belong to another group
+    for (uint64_t win = (uint64_t)wi * CWIN; win < span; win += (uint64_t)nwin * CWIN) {
         const uint64_t wend = min(span, win + (uint64_t)CWIN);
-        // ---- phase 1: chunks -> LDS image. Chunk f (flat index over the group)
-        // belongs to stream i with cpre[i] <= f < cpre[i+1].
+        const uint32_t wl = (uint32_t)(wend - win);
+        if (win != (uint64_t)wi * CWIN) {  // later windows (long streams): new chunk ranges
+            if (tid < 64) {
+                uint32_t c0 = 0, cnt = 0;
+                if (tid < ns) chunk_range(soff[tid], slen[tid], ua0, win, wend, c0, cnt);
+                publish(tid < ns, tid, c0, cnt);
+            }
+            __syncthreads();
+        }
+        const uint32_t nchunks = cpre[ns];
+        // ---- phase 1: chunks -> LDS image. Flat chunk f belongs to stream i
+        // with cpre[i] <= f < cpre[i+1].
         uint32_t si = 0;
         for (uint32_t f0 = wv * 64 * CU_LD; f0 < nchunks; f0 += 256 * CU_LD) {
             v4u v[CU_LD];
-            int64_t dpos[CU_LD];  // image position of the chunk's first byte (relative to win)
+            int32_t dpos[CU_LD];  // image position of the chunk's first byte (relative to win)
             uint32_t nv[CU_LD];   // valid bytes of the chunk
             for (uint32_t k = 0; k < CU_LD; k++) {
                 const uint32_t f = f0 + 64 * k + lane;
@@ -913,25 +959,23 @@ __global__ __launch_bounds__(256) void k_enc_compact_lds(uint8_t *enc, KArgs a, 
                 const uint8_t *src = sbase;
                 if (f < nchunks) {
                     while (cpre[si + 1] <= f) si++;
-                    const uint32_t c = f - cpre[si];
+                    const uint32_t c = clo[si] + (f - cpre[si]);
                     src = sbase + (size_t)si * w.cap + 16 * (size_t)c;
                     nv[k] = min(16u, slen[si] - 16 * c);
-                    dpos[k] = (int64_t)((uintptr_t)dbase + soff[si] + 16 * (uint64_t)c - ua0) - (int64_t)win;
-                    if (dpos[k] + 16 <= 0 || dpos[k] >= (int64_t)(wend - win)) nv[k] = 0;  // not in this window
+                    dpos[k] = (int32_t)((int64_t)((uintptr_t)dbase + soff[si] - ua0) - (int64_t)win) + 16 * (int32_t)c;
                 }
                 v[k] = *reinterpret_cast<const v4u *>(nv[k] ? src : sbase);
             }
             for (uint32_t k = 0; k < CU_LD; k++) {
                 if (!nv[k]) continue;
-                const int64_t p = dpos[k];
-                const uint32_t wl = (uint32_t)(wend - win);
-                if (nv[k] == 16 && p >= 0 && p + 16 <= (int64_t)wl && (p & 3) == 0) {
+                const int32_t p = dpos[k];
+                if (nv[k] == 16 && p >= 0 && p + 16 <= (int32_t)wl && (p & 3) == 0) {
                     uint32_t *d = reinterpret_cast<uint32_t *>(img + p);
                     d[0] = v[k].x;
                     d[1] = v[k].y;
                     d[2] = v[k].z;
                     d[3] = v[k].w;
-                } else if (nv[k] == 16 && p >= 0 && p + 20 <= (int64_t)wl) {
+                } else if (nv[k] == 16 && p >= 0 && p + 20 <= (int32_t)wl) {
                     // misaligned by a = p & 3: (4 - a) head bytes, 3 whole dwords, a tail bytes
                     const uint32_t al = (uint32_t)p & 3, sh8 = 8 * (4 - al);
                     const uint32_t w0 = v[k].x, w1 = v[k].y, w2 = v[k].z, w3 = v[k].w;
@@ -944,16 +988,15 @@ __global__ __launch_bounds__(256) void k_enc_compact_lds(uint8_t *enc, KArgs a, 
                 } else {
                     const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
                     for (uint32_t t = 0; t < nv[k]; t++) {
-                        const int64_t q = p + t;
-                        if (q >= 0 && q < (int64_t)wl) img[q] = (uint8_t)(wd[t >> 2] >> (8 * (t & 3)));
+                        const int32_t q = p + (int32_t)t;
+                        if (q >= 0 && q < (int32_t)wl) img[q] = (uint8_t)(wd[t >> 2] >> (8 * (t & 3)));
                     }
                 }
             }
         }
         __syncthreads();
         // ---- phase 2: LDS image -> destination, aligned 16-B units
-        const uint32_t nunit = (uint32_t)((wend - win + 15) / 16);
-        const uint64_t lo = (uintptr_t)dbase + r0 - ua0;  // image bytes below lo belong to another group
+        const uint32_t nunit = (wl + 15) / 16;
         for (uint32_t u = tid; u < nunit; u += 256) {
             const uint64_t q0 = win + 16 * (uint64_t)u;  // image offset of the unit
             uint8_t *dst = reinterpret_cast<uint8_t *>(ua0 + q0);
@@ -1307,8 +1350,11 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     const bool wave_all = wbase + 64 <= N;  // wave-uniform
     uint8_t *outb = raw + a.raw_off[b] + (size_t)blkF * FW;
     // output rows are addressed through a descriptor rebased every tile, so the
-    // 32-bit buffer offsets cover any buffer size
+    // 32-bit buffer offsets cover any buffer size. A lane without a stream
+    // stores at offset 2^31 (+ the row), beyond the descriptor's 2^31 - 1
+    // records: the hardware drops it, so the stores need no exec mask.
     __amdgpu_buffer_rsrc_t orsrc = byte_rsrc(outb);
+    const uint32_t voff = active ? tid : 0x80000000u;
     const uint32_t nfull = (uint32_t)((cmax - 1) / DT2);  // tiles with k0 + DT2 < cmax
     auto lov8 = [&]() -> uint32_t { return (uint32_t)lo64 << 3; };
     // lanes that fetch nothing at a boundary load a line of the table instead
@@ -1322,13 +1368,12 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if (t >= 2) {
             // wait for the loads of boundary t-2: younger are the 16 stores of tile
-            // t-2, the 4 loads of boundary t-1 and the 16 stores of tile t-1
-            if ((ABL & 1) && wave_all)
+            // t-2, the 4 loads of boundary t-1 and the 16 stores of tile t-1 (every
+            // wave issues all of them: lanes without a stream store out of range)
+            if (ABL & 1)
                 asm volatile("s_waitcnt vmcnt(4)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
-            else if (wave_all)
-                asm volatile("s_waitcnt vmcnt(36)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
             else
-                asm volatile("s_waitcnt vmcnt(0)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
+                asm volatile("s_waitcnt vmcnt(36)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
             if (pnd && ptile + 2 == t) {
                 lo64 -= 64;
                 put_seg((uint32_t)lo64, s0, s1, s2, s3);
@@ -1357,13 +1402,15 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             uint32_t hA, lA, sA, hB, lB, sB;
             const uint32_t eA = step(D, hA, lA, sA);
             const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
-            pos8 -= sA + sB - 16u;  // (v_add3 + v_sub)
+            uint32_t used;  // sA + sB - 16 = 8 * bytes consumed by the pair
+            asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
+            pos8 -= used;
             if (j + 1 < DT2 / 2) D = readD(pos8);
             if (ABL & 1) {
                 sink += eA ^ eB;
-            } else if (wave_all || active) {
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, tid, row, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eB, orsrc, tid, row + N, 0);
+            } else {  // no exec mask: a lane without a stream stores out of range (dropped)
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, voff, row, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eB, orsrc, voff, row + N, 0);
             }
             row += 2 * N;
         }
@@ -1400,10 +1447,8 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             uint32_t h, l, sf;
             const uint32_t ent = step(readD(pos8), h, l, sf);
             pos8 = pos8 + 8 - sf;
-            if (live) {
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ent, orsrc, tid, (uint32_t)(j * N), 0);
-                pos_snap = pos8;
-            }
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ent, orsrc, live ? voff : 0x80000000u, (uint32_t)(j * N), 0);
+            if (live) pos_snap = pos8;
         }
         if ((ABL & 1) && sink == 0x9E3779B9u) a.status[b] = 7;  // keeps the ablated work live
         if ((ABL & 8) && tid == 0) {
@@ -1972,9 +2017,16 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
         } else
 #endif
-        // 16 streams per workgroup, 19 KiB window (8 workgroups per CU), four 16-B loads in
-        // flight per lane (A/B: 0.140 -> 0.132 ms over two); block-sum scan fused in
-        hipLaunchKernelGGL((k_enc_compact_lds<16, 19 * 1024, 4>), dim3((uint32_t)gx * 16), dim3(256), 0, s, enc, a, w);
+        // 16 streams per group, 19 KiB windows (8 workgroups per CU), four 16-B loads in
+        // flight per lane (A/B: 0.140 -> 0.132 ms over two); block-sum scan fused in.
+        // Window workgroups per group: half the windows the group's largest
+        // possible span needs (the typical span of incompressible data), at
+        // least one; each loops over its windows
+        constexpr uint32_t CWIN = 19 * 1024;
+        const uint64_t max_span = 16ull * w.cap + 16;
+        const uint32_t nwin = (uint32_t)std::max<uint64_t>(1, max_span / CWIN / 2);
+        hipLaunchKernelGGL((k_enc_compact_lds<16, CWIN, 4>), dim3((uint32_t)(gx * 16 * nwin)), dim3(256), 0, s, enc,
+                           a, w, nwin);
         timer_end("rans_compact", s);
     }
     timer_begin("rans_encode_x1", s);
