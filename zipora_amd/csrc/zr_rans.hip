@@ -387,14 +387,27 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 // streams, e.g. one buffer x 4096, over as many CUs as it has waves).
 // ABL: diagnostic ablations, ZR_DIAG builds only (1: no scratch stores,
 // 2: conflict-free table reads); the product instantiates ABL = 0.
+//
+// LDS (one array, carved by hand so that the output ring sits at offset 0 and
+// a ring address wraps with one AND): ring 32 dwords x EW lanes | encode table
+// 256 x 16 B | input tile 16 rows x EW bytes. EW = 256: exactly 40 KiB, four
+// workgroups (16 waves) per CU.
 template <uint32_t EW, int ABL>
 __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
+    constexpr uint32_t ERS = 32;    // ring slots (dwords) per lane
+    constexpr uint32_t ETILE = 16;  // input rows (steps) per tile
+    constexpr uint32_t RING_BYTES = ERS * EW * 4;  // a power of two
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16 + ETILE * EW];
+    uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
+    uint4 *et = reinterpret_cast<uint4 *>(lds + RING_BYTES);
+    uint8_t *itile = lds + RING_BYTES + 256 * 16;
     const uint32_t nblkE = (a.N + EW - 1) / EW;
     const uint32_t b = blockIdx.x / nblkE, blk = blockIdx.x % nblkE;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
     if (single_mode(n, N)) return;
+    const uint32_t tid = threadIdx.x;
     // The state is kept as X = x << 8 | g, g < 256 an arbitrary low byte (the
     // last renorm byte): renorm tests, emitted bytes and the update all read
     // x's bits in place, and the quotient reads (X >> nb) with g cleared.
@@ -402,28 +415,24 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // one byte if > low half ((freq << 4) - 1), two if > high half ((freq << 12) - 1,
     // 0xFFFF = never, freq >= 16); y = start << 8; z = reciprocal;
     // w = (4096 - freq) << 8 | rsh << 24 (mad_u24 reads the low 24 bits)
-    __shared__ uint4 et[256];
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
-    for (uint32_t v = threadIdx.x; v < 256; v += EW) {
+    for (uint32_t v = tid; v < 256; v += EW) {
         const uint32_t f = T->freq[v];
         const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
         et[v] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
                            (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
     }
-    __syncthreads();
-    // Input rows k*N + EW*blk .. +EW-1 are staged through an LDS tile of ETILE rows:
-    // each thread moves one 16-byte piece per tile (coalesced), loaded into
+    // Input rows k*N + EW*blk .. +EW-1 are staged through the LDS tile of ETILE
+    // rows: each thread moves one 16-byte piece per tile (coalesced), loaded into
     // registers one tile ahead (the loads fly while the previous tile is coded).
-    constexpr uint32_t ETILE = 16;
-    __shared__ __attribute__((aligned(16))) uint8_t itile[ETILE * EW];
-    const uint32_t s = blk * EW + threadIdx.x;
+    const uint32_t s = blk * EW + tid;
     const bool active = s < N;
     const uint64_t c = active ? (n - s - 1) / N + 1 : 0;  // symbols s, s+N, ... < n
     const uint64_t cmax = (n - 1) / N + 1;
     const uint8_t *inb = raw + a.raw_off[b];
     const bool vec_in = ((((uintptr_t)inb) | N) & 15) == 0;
     constexpr uint32_t PPR = EW / 16;  // 16-byte pieces per row (ETILE rows x PPR = EW pieces per tile)
-    const uint32_t lr = threadIdx.x / PPR, lp = (threadIdx.x % PPR) * 16;  // my piece: row, column
+    const uint32_t lr = tid / PPR, lp = (tid % PPR) * 16;  // my piece: row, column
     auto load_piece = [&](uint64_t t) -> uint4 {
         const uint64_t k = t * ETILE + lr;
         const uint64_t p = k * N + (uint64_t)blk * EW + lp;
@@ -441,151 +450,153 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         return v;
     };
     uint32_t *out = reinterpret_cast<uint32_t *>(w.scratch + (size_t)b * w.region + (size_t)s * w.cap);
+    v4u *out4 = reinterpret_cast<v4u *>(out);
     uint32_t X = RANS_L << 8;
-    uint64_t acc = 0;               // pending output bits (emission order from bit 0)
-    uint32_t nacc = 0;              // valid bits in acc, < 32 after every push
+    uint64_t acc = 0;   // pending output bits (emission order from bit 0)
+    uint32_t nacc = 0;  // valid bits in acc, < 32 after every push
     bool err = false;
+    uint32_t xmin = 0xFFFFFFFFu;  // min F over coded symbols: 0 = a symbol not in the table
     // encode_symbol (rans.rs:303-335), branchless: at most two renorm bytes
     // (x < 2^24, xmax >= 2^12); q = x / f by the exact 24-bit reciprocal.
     // renorm bytes: x >= xmax << 8 -> 2, x >= xmax -> 1; with X = x << 8 | g,
     // x >= f << 12 <=> (X >> 16) >= f << 4 and x >= f << 20 <=> (X >> 16) >= f << 12.
     // Y = X >> nb = (x >> nb) << 8 | r (r < 256), so X' = Y + (start << 8) + q * (cmpl << 8)
-    // is x' << 8 | r.
-    uint32_t xmin = 0xFFFFFFFFu;  // min F over coded symbols: 0 = a symbol not in the table
+    // is x' << 8 | r. Returns the nb emitted bits (x's low bits, emission order).
     auto renorm_bits = [&](const uint32_t F) -> uint32_t {
         const uint32_t xh = X >> 16;
         return xh > (F >> 16) ? 16u : (xh > (F & 0xFFFFu) ? 8u : 0u);
     };
-    auto enc_fast = [&](const uint4 e) {
-        xmin = min(xmin, e.x);
-        const uint32_t nb = renorm_bits(e.x);
-        acc |= (uint64_t)__builtin_amdgcn_ubfe(X, 8, nb) << nacc;
-        nacc += nb;
+    auto enc = [&](const uint4 e, bool valid, uint32_t &nb) -> uint32_t {
+        nb = valid ? renorm_bits(e.x) : 0u;
+        const uint32_t bits = __builtin_amdgcn_ubfe(X, 8, nb);
         const uint32_t Y = X >> nb;
         const uint32_t q = __umulhi(Y & ~0xFFu, e.z) >> (e.w >> 24);  // y / f
-        X = __umul24(q, e.w) + Y + e.y;                                // (y/f)*4096 + y%f + start, << 8
-    };
-    auto enc_step = [&](const uint4 e, bool valid) {
-        err |= valid && e.x == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
-        const uint32_t nb = valid ? renorm_bits(e.x) : 0u;
-        acc |= (uint64_t)__builtin_amdgcn_ubfe(X, 8, nb) << nacc;
-        nacc += nb;
-        const uint32_t Y = X >> nb;
-        const uint32_t q = __umulhi(Y & ~0xFFu, e.z) >> (e.w >> 24);
-        const uint32_t xn = __umul24(q, e.w) + Y + e.y;
+        const uint32_t xn = __umul24(q, e.w) + Y + e.y;                // (y/f)*4096 + y%f + start, << 8
         X = valid ? xn : X;
+        return bits;
     };
-    uint32_t sc = 0;  // store instructions this wave issued since the last piece load
-    // Output: after every pair of steps the low dword of acc is written to a
-    // per-lane LDS ring ([slot][lane]: conflict-free) at slot nw, and nw
-    // advances only when that dword is complete (nacc >= 32): no branch, no
-    // register queue. At each tile boundary a lane with 16 complete dwords
-    // (64 B) pending moves them to its scratch slot in one burst of four
-    // 16-B stores, so each 64-B half of a scratch line reaches the L2 whole.
-    // A tile adds at most 8 dwords, so at most 15 + 8 are pending: 32 slots.
-    constexpr uint32_t ERS = 32;
-    __shared__ uint32_t ring[ERS * EW];
-    uint32_t nw = 0, nfl = 0;  // dwords completed / moved to scratch
-    v4u *out4 = reinterpret_cast<v4u *>(out);
-    auto push = [&]() {
-        ring[(nw & (ERS - 1)) * EW + threadIdx.x] = (uint32_t)acc;
-        nw += nacc >> 5;  // nacc < 64 here
-        acc >>= (nacc & 32);
+    // Output: after every pair of steps the low dword of acc goes to the
+    // lane's LDS ring ([slot][lane], conflict-free) at slot nw, and nw advances
+    // only when that dword is complete (nacc >= 32): no branch, no register
+    // queue. ra = the lane's ring byte address plus one ring row per completed
+    // dword, unwrapped (wrapped by one AND on use); nw32 = 32 * completed dwords.
+    // At each tile boundary a lane with 16 complete dwords (64 B) pending moves
+    // them to its scratch slot in one burst of four 16-B stores, so each 64-B
+    // half of a scratch line reaches the L2 whole. A tile adds at most 8 dwords,
+    // so at most 15 + 8 are pending: 32 slots.
+    constexpr uint32_t ROW = EW * 4;  // ring row bytes
+    uint32_t ra = tid * 4;            // + ROW * nw (mod 2^32: a multiple of RING_BYTES)
+    uint32_t nw32 = 0;                // 32 * dwords completed
+    uint32_t nfl = 0;                 // dwords moved to scratch
+    // two steps' bits (A first) -> acc, then the ring
+    auto push2 = [&](uint32_t bA, uint32_t nbA, uint32_t bB, uint32_t nbB) {
+        const uint32_t cpair = bA | (bB << nbA);  // <= 32 bits
+        acc |= (uint64_t)cpair << nacc;
+        nacc += nbA + nbB;  // < 64
+        *reinterpret_cast<uint32_t *>(lds + (ra & (RING_BYTES - 1))) = (uint32_t)acc;
+        const uint32_t t32 = nacc & 32;
+        ra += t32 * (ROW / 32);
+        nw32 += t32;
+        acc >>= t32;
         nacc &= 31;
     };
+    auto nw_of = [&]() -> uint32_t { return nw32 >> 5; };
     auto flush64 = [&]() {  // tile boundary: at most one 64-B burst per lane
-        const bool need = nw - nfl >= 16;
-        if (__builtin_amdgcn_ballot_w64(need) != 0) {  // wave-uniform
-            sc += 4;
+        const bool need = nw_of() - nfl >= 16;
+        {
             if (need) {
-                const uint32_t *r = ring + threadIdx.x;
+                // nfl is a multiple of 16: the 16 dwords are ring rows
+                // (nfl & 16) .. +15, one base address and immediate offsets
+                const uint32_t *r = ring + (nfl & 16) * EW + tid;
                 uint32_t d[16];
 #pragma unroll
-                for (int i = 0; i < 16; i++) d[i] = r[((nfl + i) & (ERS - 1)) * EW];
+                for (int i = 0; i < 16; i++) d[i] = r[i * EW];
                 const uint32_t o = nfl >> 2;
-                out4[o + 0] = v4u{d[0], d[1], d[2], d[3]};
-                out4[o + 1] = v4u{d[4], d[5], d[6], d[7]};
-                out4[o + 2] = v4u{d[8], d[9], d[10], d[11]};
-                out4[o + 3] = v4u{d[12], d[13], d[14], d[15]};
+                if (!(ABL & 1)) {
+                    out4[o + 0] = v4u{d[0], d[1], d[2], d[3]};
+                    out4[o + 1] = v4u{d[4], d[5], d[6], d[7]};
+                    out4[o + 2] = v4u{d[8], d[9], d[10], d[11]};
+                    out4[o + 3] = v4u{d[12], d[13], d[14], d[15]};
+                } else {
+                    asm volatile("" ::"v"(d[0]), "v"(d[15]));
+                }
                 nfl += 16;
             }
         }
     };
-    // piece prefetch: inline-asm loads (no compiler vmcnt(0) that would also
-    // wait for the scratch stores); the wait counts this wave's stores since.
-    auto issue_piece = [&](uint64_t t, v4u &dst) {
+    // piece prefetch: plain 16-B loads one tile ahead (the compiler's own
+    // vmcnt accounting; inline-asm loads whose destination the compiler thinks
+    // is written at issue let it reuse the register while the data is in
+    // flight)
+    auto issue_piece = [&](uint64_t t) -> v4u {
         const uint64_t k = t * ETILE + lr;
         const uint64_t p = k * N + (uint64_t)blk * EW + lp;
-        if (vec_in && k < cmax && blk * EW + lp + 16 <= N && p + 16 <= n) {
-            asm_load16(dst, (uintptr_t)(inb + p));
-        } else {
-            const uint4 v = load_piece(t);
-            dst = v4u{v.x, v.y, v.z, v.w};
-            // settle the compiler's loads here: otherwise the merge with the
-            // asm-loaded path leaves dst "pending" and the tile wait below
-            // becomes vmcnt(0), which also waits for every scratch store
-            asm volatile("" : "+v"(dst));
+        if (vec_in && k < cmax && blk * EW + lp + 16 <= N && p + 16 <= n)
+            return *reinterpret_cast<const v4u *>(inb + p);
+        const uint4 v = load_piece(t);
+        return v4u{v.x, v.y, v.z, v.w};
+    };
+    // one full tile, rows ETILE-1 .. 0, every lane a stream with all rows valid
+    auto tile_fast = [&]() {
+#pragma unroll
+        for (int g = ETILE - 4; g >= 0; g -= 4) {
+            uint32_t s3 = itile[(g + 3) * EW + tid], s2 = itile[(g + 2) * EW + tid];
+            uint32_t s1 = itile[(g + 1) * EW + tid], s0 = itile[g * EW + tid];
+            if (ABL & 2) {  // diagnostic: conflict-free table reads (consecutive entries)
+                const uint32_t t = (tid + (s0 & 1)) & 255;
+                s3 = s2 = s1 = s0 = t;
+            }
+            const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
+            xmin = min(xmin, min(min(e3.x, e2.x), min(e1.x, e0.x)));
+            uint32_t n3, n2, n1, n0;
+            const uint32_t b3 = enc(e3, true, n3);
+            const uint32_t b2 = enc(e2, true, n2);
+            push2(b3, n3, b2, n2);
+            const uint32_t b1 = enc(e1, true, n1);
+            const uint32_t b0 = enc(e0, true, n0);
+            push2(b1, n1, b0, n0);
         }
     };
     const uint64_t ntiles = (cmax + ETILE - 1) / ETILE;
-    v4u pend;
-    issue_piece(ntiles - 1, pend);
+    __syncthreads();  // the encode table
+    v4u pend = issue_piece(ntiles - 1);
+    // the tile loop, top tile first. Tiles ntiles-2 .. 1 are full for every
+    // stream and their next piece is a plain 16-B load when the workgroup's
+    // columns are all streams and the input is 16-B aligned.
+    const bool body_ok = vec_in && (uint64_t)(blk + 1) * EW <= N;  // workgroup-uniform
     for (uint64_t t = ntiles; t-- > 0;) {
         __syncthreads();
-        wait_vmcnt_le(sc, pend);  // sc is wave-uniform
         *reinterpret_cast<v4u *>(&itile[lr * EW + lp]) = pend;
         __syncthreads();
-        sc = 0;
-        if (t > 0) issue_piece(t - 1, pend);
-        if (!(ABL & 1)) flush64();
+        if (body_ok && t >= 2)
+            pend = *reinterpret_cast<const v4u *>(inb + ((t - 1) * ETILE + lr) * N + (uint64_t)blk * EW + lp);
+        else if (t > 0)
+            pend = issue_piece(t - 1);
+        flush64();
         const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
-        const bool wave_all = (uint64_t)blk * EW + (threadIdx.x & ~63u) + 64 <= N;  // wave-uniform
+        const bool wave_all = (uint64_t)blk * EW + (tid & ~63u) + 64 <= N;  // wave-uniform
         if (rtop == ETILE && t * ETILE + ETILE < cmax && wave_all) {
-            // full tile, every lane of the wave a stream: no per-lane predicates
-#pragma unroll
-            for (int g = ETILE - 4; g >= 0; g -= 4) {
-                uint32_t s3 = itile[(g + 3) * EW + threadIdx.x], s2 = itile[(g + 2) * EW + threadIdx.x];
-                uint32_t s1 = itile[(g + 1) * EW + threadIdx.x], s0 = itile[g * EW + threadIdx.x];
-                if (ABL & 2) {  // diagnostic: conflict-free table reads (consecutive entries)
-                    const uint32_t t = (threadIdx.x + (s0 & 1)) & 255;
-                    s3 = s2 = s1 = s0 = t;
-                }
-                const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
-                enc_fast(e3);
-                enc_fast(e2);
-                push();
-                enc_fast(e1);
-                enc_fast(e0);
-                push();
-            }
-        } else if (rtop == ETILE && t * ETILE + ETILE < cmax) {
-            // full tile: every row is complete for every stream (rows < cmax - 1)
-#pragma unroll
-            for (int g = ETILE - 4; g >= 0; g -= 4) {
-                const uint32_t s3 = itile[(g + 3) * EW + threadIdx.x], s2 = itile[(g + 2) * EW + threadIdx.x];
-                const uint32_t s1 = itile[(g + 1) * EW + threadIdx.x], s0 = itile[g * EW + threadIdx.x];
-                const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
-                enc_step(e3, active);
-                enc_step(e2, active);
-                push();
-                enc_step(e1, active);
-                enc_step(e0, active);
-                push();
-            }
+            tile_fast();
         } else {
+            // general tile: rows past a stream's end or lanes without a stream
+            // leave the state and emit nothing
             for (uint32_t r = rtop; r-- > 0;) {
                 const uint64_t k = t * ETILE + r;
-                const uint32_t sym = itile[r * EW + threadIdx.x];
-                enc_step(et[sym], k < c);
-                push();
+                const uint32_t sym = itile[r * EW + tid];
+                const uint4 e = et[sym];
+                const bool valid = active && k < c;
+                err |= valid && e.x == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
+                uint32_t nb;
+                const uint32_t bits = enc(e, valid, nb);
+                push2(bits, nb, 0u, 0u);
             }
         }
     }
-    wait_vmcnt_le(0, pend);
     // drain: the pending complete dwords (16-B pieces, then single dwords), then
     // the partial dword (its nacc / 8 whole bytes count)
+    const uint32_t nw = nw_of();
     {
-        const uint32_t *r = ring + threadIdx.x;
+        const uint32_t *r = ring + tid;
         while (nw - nfl >= 4) {
             out4[nfl >> 2] = v4u{r[(nfl & (ERS - 1)) * EW], r[((nfl + 1) & (ERS - 1)) * EW],
                                  r[((nfl + 2) & (ERS - 1)) * EW], r[((nfl + 3) & (ERS - 1)) * EW]};
@@ -593,26 +604,23 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         }
         for (; nfl < nw; nfl++) out[nfl] = r[(nfl & (ERS - 1)) * EW];
     }
-    const uint32_t nout = nw;
-    if (nacc) out[nout] = (uint32_t)acc;
-    const uint32_t nacc_bytes = nacc / 8;
+    if (nacc) out[nw] = (uint32_t)acc;
     if (err || xmin == 0) atomicOr(&a.status[b], 1);  // marked; converted to ZR_INVALID_INPUT by the scan
-    const uint32_t bytes = nout * 4 + nacc_bytes;
+    const uint32_t bytes = nw * 4 + nacc / 8;
     if (active) {
         w.st_state[(size_t)b * N + s] = X >> 8;
         w.st_len[(size_t)b * N + s] = bytes;
     }
     // byte sum of the 256-stream block (the unit of the offset scan); the
     // scan scratch aliases the input tile, free once every wave is past it
-    // (the LDS budget is exactly four 40 KiB workgroups per CU)
     if (EW == 256) {
         __syncthreads();
         unsigned long long *sh = reinterpret_cast<unsigned long long *>(itile);
         const uint64_t bs = block_sum(active ? bytes : 0, sh);
-        if (threadIdx.x == 0) w.blocksum[(size_t)b * w.nblk + blk] = bs;
+        if (tid == 0) w.blocksum[(size_t)b * w.nblk + blk] = bs;
     } else {  // narrow workgroups add their wave sums into the zeroed block sum
         const uint64_t ws = wave_sum(active ? bytes : 0);
-        if ((threadIdx.x & 63) == 0 && s < N)
+        if ((tid & 63) == 0 && s < N)
             atomicAdd(reinterpret_cast<unsigned long long *>(&w.blocksum[(size_t)b * w.nblk + s / 256]),
                       (unsigned long long)ws);
     }
