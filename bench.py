@@ -101,8 +101,13 @@ def cpu_baseline(data, n, B, N, threads, sample_bytes=None):
     O.lib()
     m = min(n, sample_bytes) if sample_bytes else n
 
-    def one(b, mirror=False):
-        d = data[b * n:b * n + m]
+    # pieces: whole buffers, or (sampled) consecutive m-byte slices of the buffers,
+    # each coded as its own x N stream set; up to 4 per thread
+    per = n // m
+    pieces = [b * n + i * m for b in range(B) for i in range(per)][:4 * threads]
+
+    def one(k, mirror=False):
+        d = data[pieces[k]:pieces[k] + m]
         t = _table_fast(O, d)
         if mirror:
             enc = O.rans_encode_mirror(t, N, d)
@@ -113,11 +118,11 @@ def cpu_baseline(data, n, B, N, threads, sample_bytes=None):
         assert dec == d
         return len(enc)
 
-    nb1 = min(B, 4)
-    dt1, p1 = _cpu_repeat(lambda b: one(b, True), range(nb1), 1)
-    nb = min(B, 4 * threads)  # bounded sample: up to 4 buffers per thread
+    nb1 = min(len(pieces), 4)
+    dt1, p1 = _cpu_repeat(lambda k: one(k, True), range(nb1), 1)
+    nb = len(pieces)
     dt, passes = _cpu_repeat(one, range(nb), threads)
-    what = f"{m >> 20} MiB" + (f" (first {m >> 20} MiB of each {n >> 20} MiB buffer, x{N} streams over it)"
+    what = f"{m >> 20} MiB" + (f" slices of the {n >> 20} MiB buffer(s), each its own x{N} stream set"
                                if m < n else f" buffers, x{N} streams")
     return {"value": round(passes * nb * m / 2**30 / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"all-core leg: {passes} passes over {nb} x {what} of the same uniform workload, "
@@ -200,35 +205,16 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
         fd.compress_async(raw, enc)
         fd2.decompress_async(enc, cap, out, nblk)
 
-    for _ in range(args.warmup):
-        step()
+    step()
     torch.cuda.synchronize(dev)
     clen, st = fd.result()
     dlen, st2 = fd2.result()
     if st or st2 or dlen != total or not torch.equal(out, raw):
         raise SystemExit(f"FSE warmup mismatch (status {st}/{st2}, len {dlen})")
-    L.zr_timer_reset()
-    L.zr_timer_enable(1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    L.zr_timer_enable(0)
-    dec_ms, _ = kernel_ms(L, "fse_decode")
-    enc_ms, _ = kernel_ms(L, "fse_encode")
-    hist_ms, _ = kernel_ms(L, "fse_histogram")
-    L.zr_timer_reset()
+    dt, dom, dom_ms, kms = _measure(torch, dist, world, dev, L, step, args,
+                                    ["fse_decode", "fse_encode", "fse_histogram"])
     if not torch.equal(out, raw):
         raise SystemExit("FSE decode mismatch in timed region")
-    dt = zd.max_over_ranks(dt, dev)
-    dec_bytes = clen + total
-    achieved = dec_bytes / (dec_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
     res = {
         "metric": "GiB/s encode+decode (device-resident), FSE, 256 MiB Zipf(1.1), MI355X",
         "value": round(world * total * args.steps / dt / 2**30, 3), "unit": "GiB/s", "n_gpus": world,
@@ -238,17 +224,63 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
         "config": {"workload": f"FSE 0xF6 encode+decode, 256 MiB Zipf per GPU, parallel_blocks=Some(8), "
                                f"block_size={bs >> 10} KiB ({nblk} blocks, one coder lane each)",
                    "block_size": bs, "blocks": nblk, "parallelism": f"shard{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(f"fse{bs >> 10}", "k_fse_dec")[0],
-                     "traffic_source": pmc_traffic(f"fse{bs >> 10}", "k_fse_dec")[1], "kernel": "k_fse_dec",
-                     "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
-        "kernels_ms": {"fse_decode": round(dec_ms, 4), "fse_encode": round(enc_ms, 4),
-                       "fse_histogram": round(hist_ms, 4)},
+        "roofline": _roofline(dom, dom_ms, {"fse_decode": clen + total, "fse_encode": total + clen,
+                                            "fse_histogram": total}, f"fse{bs >> 10}",
+                              {"fse_decode": "k_fse_dec", "fse_encode": "k_fse_enc", "fse_histogram": "k_fse_hist"}),
+        "kernels_ms": kms, "kernels_ms_source": KMS_SOURCE,
         "compressed_bytes": clen, "ratio": round(clen / total, 5),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_fse(host, bs, cpu_threads(args))
     return res
+
+
+RANS_SYMS = {"rans_encode": "k_enc_xn", "rans_decode": "k_dec_xn_fast", "rans_compact": "k_enc_compact_lds",
+             "histogram": "k_hist"}
+KMS_SOURCE = ("instrumented pass before the timed region (every kernel HIP-event timed); the roofline's "
+              "avg_launch_ms is the dominant kernel's, timed alone inside the timed region")
+
+
+def _roofline(dom, dom_ms, bytes_of, traffic_wl, sym):
+    """roofline object of the dominant kernel: algorithmic bytes per launch / its
+    average launch time in the timed region; traffic = PMC HBM bytes per launch."""
+    nbytes = bytes_of[dom]
+    ach = nbytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    tr, src = pmc_traffic(traffic_wl, sym[dom])
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr, "traffic_source": src,
+            "kernel": f"{sym[dom]} ({dom})", "bytes_per_launch": nbytes, "avg_launch_ms": round(dom_ms, 4)}
+
+
+def _measure(torch, dist, world, dev, L, fn, args, names):
+    """Warm up, then an instrumented pass (min(steps, 10) steps, every named
+    kernel timed) that gives kernels_ms and picks the dominant kernel, then the
+    timed region proper: args.steps steps with HIP-event timing of the dominant
+    kernel only (hipExtLaunchKernelGGL's begin/end events; each timed launch
+    still costs the queue a few us, so the other kernels run untimed there).
+    -> (seconds, dominant name, its ms per launch in the timed region, kernels_ms)"""
+    for _ in range(args.warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    select = getattr(L, "zr_timer_select", lambda names: 0)  # (older libraries in A/B runs time all)
+    L.zr_timer_reset()
+    select(b"")
+    L.zr_timer_enable(1)
+    for _ in range(max(1, min(args.steps, 10))):
+        fn()
+    torch.cuda.synchronize(dev)
+    L.zr_timer_enable(0)
+    kms = {k: round(kernel_ms(L, k)[0], 4) for k in names}
+    dominant = max(names, key=lambda k: kms[k])
+    L.zr_timer_reset()
+    select(dominant.encode())
+    L.zr_timer_enable(1)
+    dt = _timed(torch, dist, world, dev, fn, args.steps, 0)
+    L.zr_timer_enable(0)
+    dom_ms, _ = kernel_ms(L, dominant)
+    L.zr_timer_reset()
+    select(b"")
+    return dt, dominant, dom_ms, kms
 
 
 def _timed(torch, dist, world, dev, fn, steps, warmup):
@@ -333,25 +365,18 @@ def run_o1(args, torch, dist, world, rank, dev, zr, L):
         d.encode_async(raw, enc)
         d.decode_async(enc, out, n)
 
-    L.zr_timer_reset()
-    L.zr_timer_enable(1)
-    dt = _timed(torch, dist, world, dev, step, args.steps, args.warmup)
-    L.zr_timer_enable(0)
+    dt, dom, dom_ms, kms = _measure(torch, dist, world, dev, L, step, args, ["huff_o1_decode", "huff_o1_encode"])
     if not torch.equal(out, raw):
         raise SystemExit("O1 round trip mismatch")
-    ems, _ = kernel_ms(L, "huff_o1_encode")
-    dms, _ = kernel_ms(L, "huff_o1_decode")
-    ach = 2 * n / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
-    extra = {"kernels_ms": {"huff_o1_encode": round(ems, 4), "huff_o1_decode": round(dms, 4)}}
+    extra = {"kernels_ms": kms, "kernels_ms_source": KMS_SOURCE}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         extra["cpu_baseline"] = cpu_baseline_o1(host, cpu_threads(args))
     return _line("GiB/s encode+decode (device-resident), Huffman O1, 1 GiB text over 8 GPUs", world * n * args.steps
                  / dt / 2**30, world, args, dt, "synthetic (order-1 Markov text, seed per rank)",
                  {"workload": "ContextualHuffman order-1 encode+decode, 128 MiB text per GPU (1/8 of 1 GiB)",
                   "parallelism": f"shard{world}"},
-                 {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_copy16 (huff_o1_decode)",
-                  "bytes_per_launch": 2 * n, "avg_launch_ms": round(dms, 4)}, extra)
+                 _roofline(dom, dom_ms, {"huff_o1_decode": 2 * n, "huff_o1_encode": 2 * n}, "o1",
+                           {"huff_o1_decode": "k_copy16", "huff_o1_encode": "k_copy16"}), extra)
 
 
 def run_blob(args, torch, dist, world, rank, dev, zr, L):
@@ -374,30 +399,23 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
         bt.encode(raw, enc)
         bt.decode(enc, out)
 
-    L.zr_timer_reset()
-    L.zr_timer_enable(1)
-    dt = _timed(torch, dist, world, dev, step, args.steps, args.warmup)
-    L.zr_timer_enable(0)
+    dt, dom, dom_ms, kms = _measure(torch, dist, world, dev, L, step, args, ["rans_decode_x1", "rans_encode_x1"])
     bt.raise_on_error()
     if not torch.equal(out, raw):
         raise SystemExit("blob round trip mismatch")
     comp = int(bt.enc_len.sum().item())
-    dms, _ = kernel_ms(L, "rans_decode_x1")
-    ems, _ = kernel_ms(L, "rans_encode_x1")
-    extra = {"kernels_ms": {"rans_encode_x1": round(ems, 4), "rans_decode_x1": round(dms, 4)},
+    extra = {"kernels_ms": kms, "kernels_ms_source": KMS_SOURCE,
              "compressed_bytes": comp, "ratio": round(comp / total, 5)}
     if world == 1 and not args.no_host_path:
         extra.update(host_pipe_rates(zr, bt, host, [1024] * R, 1, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         extra["cpu_baseline"] = cpu_baseline_blob(host, cpu_threads(args))
-    ach = (comp + total) / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
     return _line("GiB/s encode+decode (device-resident), rANS x1 record batch, 1 M x 1 KiB", world * total *
                  args.steps / dt / 2**30, world, args, dt, "synthetic (order-1 Markov text records)",
                  {"workload": f"{R} x 1 KiB records per GPU, rANS x1 per record, shared trained table",
                   "records": R, "parallelism": f"shard{world}"},
-                 {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_dec_x1 (rans_decode_x1)",
-                  "bytes_per_launch": comp + total, "avg_launch_ms": round(dms, 4)}, extra)
+                 _roofline(dom, dom_ms, {"rans_decode_x1": comp + total, "rans_encode_x1": total + comp}, "blob",
+                           {"rans_decode_x1": "k_dec_x1_ring", "rans_encode_x1": "k_enc_x1_fast"}), extra)
 
 
 
@@ -408,7 +426,8 @@ def host_pipe_rates(zr, bt, host, lens, N, steps):
     import torch
     from zipora_amd.device import RansHostPipe
     lens = np.asarray(lens, dtype=np.uint64)  # converted once, outside the timed calls
-    hist = [int(v) for v in bt.hist[:256].cpu().tolist()]
+    # the shared table of the whole batch (the device step consumes bt.hist)
+    hist = [int(v) for v in np.bincount(np.frombuffer(host, dtype=np.uint8), minlength=256)]
     pipe = RansHostPipe(zr.Rans64Encoder(hist, N).table, N)
     raw_off, _, rb, eb = pipe.layout(lens)
     pin = torch.empty(rb, dtype=torch.uint8, pin_memory=True)
@@ -477,59 +496,35 @@ def main():
     out = bt.new_raw()
     stream = torch.cuda.current_stream(dev)
 
+    # hist starts zeroed (allocation) and the consuming table build re-zeroes it,
+    # so the step carries no memset (A/B runs against an older library, which
+    # lacks the consuming entry point, memset instead)
+    consume = hasattr(L, "zr_rans_dtab_from_hist_consume_dev")
+
     def step():
-        bt.histogram(raw, stream)
+        bt.histogram(raw, stream, zeroed=consume)
         if world > 1:  # the shared frequency table: RCCL all-reduce of 256 counts
             zd.allreduce_histogram(bt.hist)
-        bt.tables_from_hist(stream)
+        bt.tables_from_hist(stream, consume=consume)
         bt.encode(raw, enc, stream)
         bt.decode(enc, out, stream)
 
-    for _ in range(args.warmup):
-        step()
+    step()
     torch.cuda.synchronize(dev)
     if not diag:
         bt.raise_on_error()
         if not torch.equal(out, raw):
-            raise SystemExit("decode mismatch after warmup")
+            raise SystemExit("decode mismatch after the first step")
 
-    L.zr_timer_reset()
-    L.zr_timer_enable(1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    L.zr_timer_enable(0)
-
-    def kt(name):
-        return kernel_ms(L, name)
-
-    dec_ms, dec_n = kt("rans_decode")
-    enc_ms, _ = kt("rans_encode")
-    cmp_ms, _ = kt("rans_compact")
-    hist_ms, _ = kt("histogram")
-    L.zr_timer_reset()
+    dt, dom, dom_ms, kms = _measure(torch, dist, world, dev, L, step, args,
+                                    ["rans_encode", "rans_decode", "rans_compact", "histogram"])
 
     if not diag:
         bt.raise_on_error()
         if not torch.equal(out, raw):
             raise SystemExit("decode mismatch in timed region")
     comp_bytes = int(bt.enc_len.sum().item())
-
-    dt = zd.max_over_ranks(dt, dev)
     value = world * total * args.steps / dt / 2**30
-
-    # dominant kernel: the fast decode (reads C compressed bytes, writes N_in bytes)
-    dec_bytes = comp_bytes + total
-    achieved = dec_bytes / (dec_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
-    kms = {"rans_decode": round(dec_ms, 4), "rans_encode": round(enc_ms, 4),
-           "rans_compact": round(cmp_ms, 4), "histogram": round(hist_ms, 4)}
     if diag:  # tools/*.sh read the kernel times; no metric from a diagnostic build
         if rank == 0:
             print(json.dumps({"diagnostic": diag, "kernels_ms": kms, "ms_per_step": round(dt / args.steps * 1e3, 4)}),
@@ -537,6 +532,8 @@ def main():
         return
     literal = B == 1
     wl = "rans_literal" if literal else "rans"
+    rans_bytes = {"rans_encode": total + comp_bytes, "rans_decode": comp_bytes + total,
+                  "rans_compact": 2 * comp_bytes, "histogram": total}
 
     res = {
         "metric": "GiB/s encode+decode (device-resident), rANS O0, 256 MiB, 1/2/4/8 MI355X",
@@ -558,20 +555,19 @@ def main():
                                 f"{B} x {n >> 20} MiB buffers, {N}-way interleaved streams each "
                                 f"({B * N} streams), shared table (histogram all-reduce over ranks)"),
                    "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic(wl, "k_dec_xn_fast")[0],
-                     "traffic_source": pmc_traffic(wl, "k_dec_xn_fast")[1],
-                     "kernel": "k_dec_xn_fast (rans_decode)",
-                     "bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
-        "kernels_ms": kms,
+        # the dominant kernel's roofline (the encoder on the headline): algorithmic bytes
+        # per launch = N_in read + C written (encode, decode), 2 C (compaction), N_in (histogram)
+        "roofline": _roofline(dom, dom_ms, rans_bytes, wl, RANS_SYMS),
+        # the decoder's, from the instrumented pass (the decode half of the step)
+        "roofline_decode": _roofline("rans_decode", kms["rans_decode"], rans_bytes, wl, RANS_SYMS),
+        "kernels_ms": kms, "kernels_ms_source": KMS_SOURCE,
         "compressed_bytes": comp_bytes,
         "ratio": round(comp_bytes / total, 5),
     }
     if rank == 0 and world == 1 and not args.no_host_path:
         res.update(host_pipe_rates(zr, bt, host, [n] * B, N, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # literal config: the first 16 MiB of the buffer as its own x4096 stream set
+        # literal config: 16 MiB slices of the buffer, each its own x4096 stream set
         res["cpu_baseline"] = cpu_baseline(host, n, B, N, cpu_threads(args),
                                            sample_bytes=(16 << 20) if literal else None)
     if rank == 0:

@@ -119,6 +119,10 @@ int32_t zr_histogram_dev(const uint8_t *raw, const zr_rans_batch *batch, int32_t
 /* Rans64Encoder::new on device, one table per histogram (no host round trip) */
 int32_t zr_rans_dtab_from_hist_dev(const uint32_t *hist_dev, uint32_t n_tables, void *dtabs_dev,
                                    void *stream);
+/* the same, then zeroes the histograms it read (stream-ordered), so the next
+ * accumulating zr_histogram_dev into them needs no zr_memset_dev */
+int32_t zr_rans_dtab_from_hist_consume_dev(uint32_t *hist_dev, uint32_t n_tables, void *dtabs_dev,
+                                           void *stream);
 /* bytes of device workspace needed by encode/decode of this batch geometry */
 size_t zr_rans_workspace_bytes(uint32_t n_buffers, uint32_t n_streams, uint64_t max_len);
 /* batched Rans64Encoder::encode: raw -> enc (enc + enc_off[b] must hold
@@ -361,6 +365,8 @@ int32_t zr_stream_sync(void *stream);
  * kernel on the stream it is launched on ("rans_decode", "rans_encode",
  * "fse_decode", ...). read() synchronises those events. */
 int32_t zr_timer_enable(int32_t on);
+/* time only the named kernels (comma-separated, e.g. "rans_encode"); NULL or "" = all */
+int32_t zr_timer_select(const char *names);
 int32_t zr_timer_reset(void);
 int32_t zr_timer_read(const char *kernel, double *total_ms, uint64_t *launches);
 

@@ -108,6 +108,73 @@ def test_rans_narrow_shape_ragged(zr, oracle, N):
         assert bt.raw_of(out, b) == d
 
 
+def test_status_written_without_zeroing(zr, oracle):
+    """encode/decode write every buffer's status themselves (no memset in the
+    call): xN and x1 buffers, an empty one, a symbol missing from its table
+    (rans.rs:311-316) and a header shorter than min_header_size
+    (rans.rs:563-568), over a status array pre-filled with garbage."""
+    import torch
+    from zipora_amd._lib import ZR_INVALID_INPUT
+    from zipora_amd.device import RansDeviceBatch
+    N = 64
+    lens = [0, 10, 5000, 5000, 70000]
+    datas = [b"", bytes(range(10)), zr.synth("t", 5000, seed=3), b"ab" * 2500, zr.synth("u", 70000, seed=4)]
+    bt = RansDeviceBatch(lens, N, shared_table=False)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.histogram(raw)
+    bt.tables_from_hist(consume=True)
+    assert int(bt.hist.abs().sum().item()) == 0  # consumed
+    raw[bt.raw_off_host[3] + 7] = 0xFF  # not in buffer 3's table
+    bt.status.fill_(12345)
+    bt.encode(raw, enc)
+    torch.cuda.synchronize()
+    assert bt.statuses() == [0, 0, 0, ZR_INVALID_INPUT, 0]
+    for b in (0, 1, 2, 4):
+        t = oracle.rans_table(oracle.histogram(datas[b]))
+        assert bt.encoded(enc, b) == oracle.rans_encode(t, N, datas[b]), f"buffer {b}"
+    bt.enc_len[2] = 5      # shorter than the N * 12 header
+    bt.enc_len[3] = 0
+    bt.status.fill_(-7)
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    assert bt.statuses() == [0, 0, ZR_INVALID_INPUT, ZR_INVALID_INPUT, 0]
+    for b in (0, 1, 4):
+        assert bt.raw_of(out, b) == datas[b]
+
+
+@pytest.mark.parametrize("nzero", [1, 16])
+def test_rans_generic_fallback_lanes(zr, oracle, nzero):
+    """Streams the fast decoder cannot hold: a shared table in which almost every
+    byte but 0 has frequency 1 (rans.rs:238-299 on a batch dominated by zeros), so a
+    buffer of bytes 1..255 costs ~1.5 bytes per symbol and its lanes outrun their
+    LDS rings; they fall back to the generic per-lane decoder inside the same
+    kernel. One-wave (nzero=1) and 1024-lane (nzero=16) workgroups."""
+    import numpy as np
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    N, n = 4096, 256 << 10
+    rnd = np.random.default_rng(7)
+    hard = bytes(rnd.integers(1, 256, n, dtype=np.uint8))
+    datas = [bytes(4 << 20)] * nzero + [hard]
+    bt = RansDeviceBatch([len(d) for d in datas], N, shared_table=True)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    t = oracle.rans_table(oracle.histogram(b"".join(datas)))
+    assert sum(f == 1 for f in t.freq[1:]) >= 250  # (pass 3 gives the remainder to one of them)
+    assert bt.encoded(enc, nzero) == oracle.rans_encode(t, N, hard)
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    for b, d in enumerate(datas):
+        assert bt.raw_of(out, b) == d, f"buffer {b}"
+
+
 def _dtab_words(bt, k=0):
     w = bt.tables.cpu().numpy().view(np.uint32)
     per = bt.tables.numel() // 4 // bt.n_tables

@@ -80,6 +80,7 @@ SIGNATURES = [
     ("zr_rans_dtab_upload", ctypes.c_int32, [ctypes.POINTER(RansTable), ctypes.c_uint32, c_vp, c_vp]),
     ("zr_histogram_dev", ctypes.c_int32, [c_vp, ctypes.POINTER(RansBatch), ctypes.c_int32, c_vp, c_vp]),
     ("zr_rans_dtab_from_hist_dev", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp]),
+    ("zr_rans_dtab_from_hist_consume_dev", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp]),
     ("zr_rans_workspace_bytes", c_sz, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     ("zr_rans_encode_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp, c_sz,
                                                   c_vp]),
@@ -172,6 +173,7 @@ SIGNATURES = [
     ("zr_memset_dev", ctypes.c_int32, [c_vp, ctypes.c_int, c_sz, c_vp]),
     ("zr_stream_sync", ctypes.c_int32, [c_vp]),
     ("zr_timer_enable", ctypes.c_int32, [ctypes.c_int32]),
+    ("zr_timer_select", ctypes.c_int32, [ctypes.c_char_p]),
     ("zr_timer_reset", ctypes.c_int32, []),
     ("zr_timer_read", ctypes.c_int32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_uint64)]),

@@ -471,8 +471,12 @@ struct TimerRec {
 };
 std::mutex g_tm;
 bool g_timer_on = false;
+std::string g_sel;  // ",name,name," : the timed kernels; empty = all
 std::vector<TimerRec> g_recs;
 std::vector<hipEvent_t> g_pool;
+bool selected(const char *name) {
+    return g_sel.empty() || g_sel.find("," + std::string(name) + ",") != std::string::npos;
+}
 hipEvent_t ev_get() {
     if (!g_pool.empty()) {
         hipEvent_t e = g_pool.back();
@@ -485,16 +489,23 @@ hipEvent_t ev_get() {
 }
 }  // namespace
 
+TimerPair timer_pair(const char *name) {
+    std::lock_guard<std::mutex> g(g_tm);
+    if (!g_timer_on || !selected(name)) return TimerPair{nullptr, nullptr};
+    TimerRec r{name, ev_get(), ev_get()};
+    g_recs.push_back(r);
+    return TimerPair{r.a, r.b};
+}
 void timer_begin(const char *name, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_tm);
-    if (!g_timer_on) return;
+    if (!g_timer_on || !selected(name)) return;
     TimerRec r{name, ev_get(), ev_get()};
     (void)hipEventRecord(r.a, s);
     g_recs.push_back(r);
 }
 void timer_end(const char *name, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_tm);
-    if (!g_timer_on) return;
+    if (!g_timer_on || !selected(name)) return;
     for (auto it = g_recs.rbegin(); it != g_recs.rend(); ++it)
         if (it->name == name) {
             (void)hipEventRecord(it->b, s);
@@ -507,6 +518,18 @@ extern "C" {
 int32_t zr_timer_enable(int32_t on) {
     std::lock_guard<std::mutex> g(g_tm);
     g_timer_on = on != 0;
+    // events are created here, not per launch inside a timed region
+    while (g_timer_on && g_pool.size() + 2 * g_recs.size() < 1024) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) break;
+        g_pool.push_back(e);
+    }
+    return ZR_OK;
+}
+int32_t zr_timer_select(const char *names) {
+    std::lock_guard<std::mutex> g(g_tm);
+    g_sel.clear();
+    if (names && *names) g_sel = "," + std::string(names) + ",";
     return ZR_OK;
 }
 int32_t zr_timer_reset(void) {

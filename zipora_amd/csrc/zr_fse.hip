@@ -1018,15 +1018,11 @@ int32_t zr_fse_compress_dev(const zr_fse_config *c, const uint32_t *freqs_dev, c
         hist = const_cast<uint32_t *>(freqs_dev);
     } else {
         ZR_HIP(hipMemsetAsync(hist, 0, 1024, s));
-        timer_begin("fse_histogram", s);
-        hipLaunchKernelGGL(k_fse_hist, dim3((uint32_t)ceil_div(n, FH_CHUNK)), dim3(256), 0, s, in, (uint64_t)n,
-                           hist);
-        timer_end("fse_histogram", s);
+        launch_timed("fse_histogram", k_fse_hist, dim3((uint32_t)ceil_div(n, FH_CHUNK)), dim3(256), 0, s, in,
+                     (uint64_t)n, hist);
     }
     hipLaunchKernelGGL(k_fse_tab, dim3(1), dim3(256), 0, s, hist, tab);
-    timer_begin("fse_encode", s);
-    hipLaunchKernelGGL(k_fse_enc, dim3((uint32_t)ceil_div(p.nb, 64)), dim3(64), 0, s, a);
-    timer_end("fse_encode", s);
+    launch_timed("fse_encode", k_fse_enc, dim3((uint32_t)ceil_div(p.nb, 64)), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_fse_scan, dim3(1), dim3(256), 0, s, a.body, p.nb, p.mode, out, boff, out_len_dev,
                        status_dev, tab);
     hipLaunchKernelGGL(k_fse_compact, dim3((uint32_t)p.nb), dim3(256), 0, s, a, out, boff);
@@ -1068,9 +1064,7 @@ int32_t zr_fse_decompress_dev(const uint8_t *in, size_t n, uint8_t *out, size_t 
     hipLaunchKernelGGL(k_fse_parse, dim3(gb), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_fse_tabs, dim3(gb), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_fse_outscan, dim3(1), dim3(256), 0, s, a);
-    timer_begin("fse_decode", s);
-    hipLaunchKernelGGL(k_fse_dec, dim3((uint32_t)ceil_div(max_blocks, 64)), dim3(64), 0, s, a);
-    timer_end("fse_decode", s);
+    launch_timed("fse_decode", k_fse_dec, dim3((uint32_t)ceil_div(max_blocks, 64)), dim3(64), 0, s, a);
     ZR_HIP(hipGetLastError());
     return ZR_OK;
     ZR_GUARD_END

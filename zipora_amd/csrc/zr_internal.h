@@ -1,6 +1,7 @@
 // zr_internal.h -- shared definitions of the MI355X entropy backend (product code).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 #include <string>
@@ -38,6 +39,8 @@ void clear_error();
 constexpr uint32_t RANS_L = 1u << 16;
 constexpr uint32_t TF_SHIFT = 12;
 constexpr uint32_t TOTFREQ = 1u << TF_SHIFT;
+// top bit of an encoder block byte sum: a symbol of the block is not in the table
+constexpr uint64_t BS_ERR = 1ull << 63;
 
 // Device table: everything the encode and decode kernels need for one
 // normalised frequency table. 16-byte aligned, copied into LDS per workgroup.
@@ -79,7 +82,6 @@ struct RansWork {
     uint32_t *st_len;     // [B*N]
     uint64_t *blocksum;   // [B*nblk]
     uint64_t *blockoff;   // [B*nblk]
-    uint32_t *redo;       // [B*nblk]
     uint8_t *scratch;     // [B*R]
     uint64_t region;      // R: scratch bytes per buffer
     uint32_t cap;         // scratch bytes per stream (xN mode)
@@ -88,8 +90,22 @@ struct RansWork {
 size_t rans_workspace_bytes(uint32_t B, uint32_t N, uint64_t max_len);
 int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t bytes, RansWork *w);
 
-// HIP-event timing of named kernels (zr_timer_* in the C ABI). When enabled,
-// launchers bracket the named kernel with events recorded on its own stream.
+// HIP-event timing of named kernels (zr_timer_* in the C ABI).
+// launch_timed: one kernel launch whose own begin/end the dispatch records in
+// a pair of HIP events (hipExtLaunchKernelGGL). No marker packets enter the
+// stream: a separate hipEventRecord costs the MI355X queue about 5 us of idle
+// per event, 40 us per headline step with four timed kernels.
+// timer_begin/timer_end bracket a multi-kernel range with recorded events.
+struct TimerPair {
+    hipEvent_t a, b;
+};
+TimerPair timer_pair(const char *name);  // {nullptr, nullptr} while timers are off
+template <typename F, typename... Args>
+inline void launch_timed(const char *name, F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s,
+                         Args... args) {
+    const TimerPair t = timer_pair(name);
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, t.a, t.b, 0u, args...);
+}
 void timer_begin(const char *name, hipStream_t s);
 void timer_end(const char *name, hipStream_t s);
 

@@ -229,13 +229,16 @@ __global__ __launch_bounds__(256) void k_hist_small(const uint8_t *raw, KArgs a,
 // table build on device: Rans64Encoder::new (rans.rs:208-235) with
 // normalize_frequencies (rans.rs:238-299) and the symbol starts (rans.rs:225-228)
 // ======================================================================
-__global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tabs) {
+// clear: non-null = the histogram itself, zeroed once read (each thread its own
+// bin), so the next accumulating zr_histogram_dev needs no memset
+__global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tabs, uint32_t *clear) {
     __shared__ unsigned long long sh[4];
     __shared__ uint32_t norm_s[256], start_s[256], freq_raw[256];
     __shared__ unsigned long long best;
     const uint32_t v = threadIdx.x;
     RansDTab *d = tabs + blockIdx.x;
     const uint32_t f = hist[(size_t)blockIdx.x * 256 + v];
+    if (clear) clear[(size_t)blockIdx.x * 256 + v] = 0;
     freq_raw[v] = f;
     // total_freq: u32 wrapping sum (rans.rs:209)
     const uint32_t total = (uint32_t)block_sum(f, sh);
@@ -432,18 +435,19 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     const uint8_t *inb = raw + a.raw_off[b];
     const bool vec_in = ((((uintptr_t)inb) | N) & 15) == 0;
     constexpr uint32_t PPR = EW / 16;  // 16-byte pieces per row (ETILE rows x PPR = EW pieces per tile)
-    const uint32_t lr = tid / PPR, lp = (tid % PPR) * 16;  // my piece: row, column
+    const uint32_t lr = tid / PPR, lp = (tid % PPR) * 16;  // my piece: row, column in the tile
+    const uint32_t col = blk * EW + lp;                    // and its stream (column of the buffer)
     auto load_piece = [&](uint64_t t) -> uint4 {
         const uint64_t k = t * ETILE + lr;
-        const uint64_t p = k * N + (uint64_t)blk * EW + lp;
+        const uint64_t p = k * N + col;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < cmax && blk * EW + lp < N) {
+        if (k < cmax && col < N) {
             if (vec_in && p + 16 <= n) {
                 v = *reinterpret_cast<const uint4 *>(inb + p);
             } else {
                 uint32_t wv[4] = {0, 0, 0, 0};
                 for (uint32_t j = 0; j < 16; j++)
-                    if (p + j < n && blk * EW + lp + j < N) wv[j >> 2] |= (uint32_t)inb[p + j] << (8 * (j & 3));
+                    if (p + j < n && col + j < N) wv[j >> 2] |= (uint32_t)inb[p + j] << (8 * (j & 3));
                 v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
             }
         }
@@ -530,8 +534,8 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // flight)
     auto issue_piece = [&](uint64_t t) -> v4u {
         const uint64_t k = t * ETILE + lr;
-        const uint64_t p = k * N + (uint64_t)blk * EW + lp;
-        if (vec_in && k < cmax && blk * EW + lp + 16 <= N && p + 16 <= n)
+        const uint64_t p = k * N + col;
+        if (vec_in && k < cmax && col + 16 <= N && p + 16 <= n)
             return *reinterpret_cast<const v4u *>(inb + p);
         const uint4 v = load_piece(t);
         return v4u{v.x, v.y, v.z, v.w};
@@ -564,17 +568,30 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // stream and their next piece is a plain 16-B load when the workgroup's
     // columns are all streams and the input is 16-B aligned.
     const bool body_ok = vec_in && (uint64_t)(blk + 1) * EW <= N;  // workgroup-uniform
+    const bool wave_all = (uint64_t)blk * EW + (tid & ~63u) + 64 <= N;  // wave-uniform
+    // A one-wave workgroup (EW = 64) needs no barrier: a wave's LDS accesses
+    // complete in program order (the fences pin the compiler). Wider
+    // workgroups keep the shared tile: wave-private 64-column tiles split each
+    // 128-B input line between two waves that drift apart, and measured 30 %
+    // more FETCH and a slower encode.
+    auto tile_sync = [&]() {
+        if (EW > 64) {
+            __syncthreads();
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
     for (uint64_t t = ntiles; t-- > 0;) {
-        __syncthreads();
+        tile_sync();
         *reinterpret_cast<v4u *>(&itile[lr * EW + lp]) = pend;
-        __syncthreads();
+        tile_sync();
         if (body_ok && t >= 2)
-            pend = *reinterpret_cast<const v4u *>(inb + ((t - 1) * ETILE + lr) * N + (uint64_t)blk * EW + lp);
+            pend = *reinterpret_cast<const v4u *>(inb + ((t - 1) * ETILE + lr) * N + col);
         else if (t > 0)
             pend = issue_piece(t - 1);
         flush64();
         const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
-        const bool wave_all = (uint64_t)blk * EW + (tid & ~63u) + 64 <= N;  // wave-uniform
         if (rtop == ETILE && t * ETILE + ETILE < cmax && wave_all) {
             tile_fast();
         } else {
@@ -605,7 +622,9 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         for (; nfl < nw; nfl++) out[nfl] = r[(nfl & (ERS - 1)) * EW];
     }
     if (nacc) out[nw] = (uint32_t)acc;
-    if (err || xmin == 0) atomicOr(&a.status[b], 1);  // marked; converted to ZR_INVALID_INPUT by the scan
+    // "Symbol {} not in frequency table" (rans.rs:311-316): flagged in the top bit
+    // of the block's byte sum (BS_ERR); the compaction turns it into the status
+    const bool bad = err || xmin == 0;
     const uint32_t bytes = nw * 4 + nacc / 8;
     if (active) {
         w.st_state[(size_t)b * N + s] = X >> 8;
@@ -615,14 +634,19 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // scan scratch aliases the input tile, free once every wave is past it
     if (EW == 256) {
         __syncthreads();
+        // one reduction (no extra LDS: the workgroup's 40 KiB are exact for four
+        // per CU): bytes (< 2^40) and, from bit 55, the count of lanes in error
         unsigned long long *sh = reinterpret_cast<unsigned long long *>(itile);
-        const uint64_t bs = block_sum(active ? bytes : 0, sh);
-        if (tid == 0) w.blocksum[(size_t)b * w.nblk + blk] = bs;
+        const uint64_t r = block_sum((active ? bytes : 0) | ((uint64_t)bad << 55), sh);
+        if (tid == 0) w.blocksum[(size_t)b * w.nblk + blk] = (r & ((1ull << 55) - 1)) | ((r >> 55) ? BS_ERR : 0);
     } else {  // narrow workgroups add their wave sums into the zeroed block sum
         const uint64_t ws = wave_sum(active ? bytes : 0);
-        if ((tid & 63) == 0 && s < N)
-            atomicAdd(reinterpret_cast<unsigned long long *>(&w.blocksum[(size_t)b * w.nblk + s / 256]),
-                      (unsigned long long)ws);
+        const bool wbad = __any(bad);
+        if ((tid & 63) == 0 && s < N) {
+            unsigned long long *t = reinterpret_cast<unsigned long long *>(&w.blocksum[(size_t)b * w.nblk + s / 256]);
+            atomicAdd(t, (unsigned long long)ws);
+            if (wbad) atomicOr(t, (unsigned long long)BS_ERR);
+        }
     }
 }
 
@@ -655,7 +679,7 @@ __global__ __launch_bounds__(64) void k_enc_x1_generic(const uint8_t *raw, KArgs
         const uint32_t q = __umulhi(x << 8, T->rcp[sym]) >> T->rsh[sym];
         x = x + T->start[sym] + q * (TOTFREQ - f);
     }
-    if (err) a.status[b] = ZR_INVALID_INPUT;
+    a.status[b] = err ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an x1 buffer's encode
     w.st_state[(size_t)b * a.N] = x;
     w.blocksum[(size_t)b * w.nblk] = no;  // x1: renorm byte count
     a.enc_len[b] = no + 8;
@@ -671,9 +695,12 @@ __global__ __launch_bounds__(256) void k_scan(KArgs a, RansWork w, int decode) {
     __shared__ unsigned long long sh[4];
     const uint32_t nblk = w.nblk;
     uint64_t carry = 0;
+    int bad = 0;
     for (uint32_t base = 0; base < nblk; base += 256) {
         const uint32_t i = base + threadIdx.x;
-        const uint64_t v = i < nblk ? w.blocksum[(size_t)b * nblk + i] : 0;
+        const uint64_t raw_v = i < nblk ? w.blocksum[(size_t)b * nblk + i] : 0;
+        bad = __syncthreads_or(bad || (raw_v & BS_ERR));
+        const uint64_t v = raw_v & ~BS_ERR;
         uint64_t tot;
         const uint64_t ex = block_excl_scan(v, sh, &tot);
         if (i < nblk) w.blockoff[(size_t)b * nblk + i] = carry + ex;
@@ -683,7 +710,7 @@ __global__ __launch_bounds__(256) void k_scan(KArgs a, RansWork w, int decode) {
         const uint64_t hdr = (uint64_t)N * 12;
         if (!decode) {
             a.enc_len[b] = hdr + carry;
-            if (a.status[b] != 0) a.status[b] = ZR_INVALID_INPUT;
+            a.status[b] = bad ? ZR_INVALID_INPUT : ZR_OK;
         } else if (a.status[b] == 0 && hdr + carry > a.enc_len[b]) {
             a.status[b] = ZR_INVALID_INPUT;  // "Invalid stream data length" (rans.rs:608-610)
         }
@@ -852,21 +879,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
     // the buffer's scan of block byte sums (k_scan, fused): this block's
     // offset, and for group 0 the encoded length and the final status
-    uint64_t below = 0, all = 0;
+    uint64_t below = 0, all = 0, flagged = 0;
     for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
         const uint64_t v = w.blocksum[(size_t)b * nblk + i];
-        below += i < blk ? v : 0;
-        all += v;
+        const uint64_t c = v & ~BS_ERR;
+        below += i < blk ? c : 0;
+        all += c;
+        flagged |= v >> 63;
     }
-    const uint64_t bo = block_sum(below, sh);
-    if (grp == 0 && wi == 0) {  // workgroup-uniform
+    // one reduction: the bytes below this block (< 2^55), and above them the
+    // number of threads that saw a block flagged by k_enc_xn
+    const uint64_t r = block_sum(below | (flagged << 55), sh);
+    const uint64_t bo = r & ((1ull << 55) - 1);
+    const bool failed = (r >> 55) != 0;
+    if (grp == 0 && wi == 0) {  // workgroup-uniform: the buffer's status and length
         const uint64_t tot = block_sum(all, sh);
         if (threadIdx.x == 0) {
             a.enc_len[b] = (uint64_t)N * 12 + tot;
-            if (a.status[b] != 0) a.status[b] = ZR_INVALID_INPUT;
+            a.status[b] = failed ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an xN encode
         }
     }
-    if (a.status[b] != 0) return;  // nonzero for every reader once marked by k_enc_xn
+    if (failed) return;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wv = tid >> 6;
     uint8_t *dbase = enc + a.enc_off[b] + 12 * (size_t)N;
@@ -1039,159 +1072,8 @@ __global__ __launch_bounds__(256) void k_dec_hdr(const uint8_t *enc, KArgs a, Ra
     const uint64_t bs = block_sum(L, sh);
     if (threadIdx.x == 0) {
         w.blocksum[(size_t)b * nblk + blk] = bs;
-        w.redo[(size_t)b * nblk + blk] = 0;
-        if (!hdr_ok && blk == 0) a.status[b] = ZR_INVALID_INPUT;
+        if (blk == 0) a.status[b] = hdr_ok ? ZR_OK : ZR_INVALID_INPUT;  // the decode's first status write
     }
-}
-
-constexpr int TILE = 16;  // decode steps staged per LDS tile
-
-// Writes rows [k0, k0+rows) of the staged tile to raw (row k -> raw[k*N + 256*blk ...]).
-__device__ __forceinline__ void flush_tile(const uint8_t *tile, uint8_t *outb, uint64_t n, uint32_t N,
-                                           uint32_t blk, uint64_t k0, uint32_t rows, bool vec_ok) {
-    const uint32_t col0 = blk * 256;
-    const uint32_t width = min(256u, N - col0);
-    if (vec_ok && width == 256) {
-        // 16 threads per row, 16 bytes each
-        const uint32_t r = threadIdx.x >> 4, cc = (threadIdx.x & 15) * 16;
-        if (r < rows) {
-            const uint64_t k = k0 + r;
-            const uint64_t rowbase = k * N + col0;
-            if (rowbase + 256 <= n) {
-                *reinterpret_cast<uint4 *>(outb + rowbase + cc) =
-                    *reinterpret_cast<const uint4 *>(tile + r * 256 + cc);
-            } else {
-                for (uint32_t j = 0; j < 16; j++)
-                    if (rowbase + cc + j < n) outb[rowbase + cc + j] = tile[r * 256 + cc + j];
-            }
-        }
-    } else {
-        const uint32_t t = threadIdx.x;
-        if (t < width) {
-            for (uint32_t r = 0; r < rows; r++) {
-                const uint64_t pos = (k0 + r) * N + col0 + t;
-                if (pos < n) outb[pos] = tile[r * 256 + t];
-            }
-        }
-    }
-}
-
-// Fast path: 32-bit state in [2^16, 2^24), packed LDS slot table, 64-bit MSB-first
-// register window over the stream bytes refilled by aligned dword loads.
-// GENERIC: u64 state, any table kind, byte-wise renormalisation exactly as
-// decode_symbol (rans.rs:472-507). Workgroups the fast path cannot take are
-// flagged in w.redo and re-run by the GENERIC instance.
-template <bool GENERIC>
-__global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w) {
-    const uint32_t nblk = w.nblk;
-    const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
-    if (b >= a.B) return;
-    const uint64_t n = a.len[b];
-    const uint32_t N = a.N;
-    if (n == 0 || single_mode(n, N) || a.status[b] != 0) return;
-    if (GENERIC && !w.redo[(size_t)b * nblk + blk]) return;
-    __shared__ uint32_t stab[TOTFREQ];
-    __shared__ uint8_t tile[TILE * 256];
-    __shared__ unsigned long long sh[4];
-    __shared__ uint32_t gfreq[GENERIC ? 256 : 1], gstart[GENERIC ? 256 : 1];
-    const RansDTab *T = tab_for(a.tables, a.table_stride, b);
-    for (uint32_t j = threadIdx.x; j < TOTFREQ; j += 256) stab[j] = T->slot[j];
-    if (GENERIC) {
-        gfreq[threadIdx.x] = T->freq[threadIdx.x];
-        gstart[threadIdx.x] = T->start[threadIdx.x];
-    }
-    const uint32_t kind = T->kind;
-    const uint32_t s = blk * 256 + threadIdx.x;
-    const bool active = s < N;
-    const uint8_t *e = enc + a.enc_off[b];
-    const uint32_t L = active ? ld_u32_u(e + 8 * (size_t)N + 4 * (size_t)s) : 0;
-    const uint64_t off = block_excl_scan(L, sh, nullptr) + w.blockoff[(size_t)b * nblk + blk];
-    uint64_t X = active ? ld_u64_u(e + 8 * (size_t)s) : RANS_L;
-    if (!GENERIC) {
-        const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24);
-        if (__syncthreads_or(!fast)) {
-            if (threadIdx.x == 0) w.redo[(size_t)b * nblk + blk] = 1;
-            return;
-        }
-    }
-    __syncthreads();
-    const uint64_t c = active ? (n - s - 1) / N + 1 : 0;
-    const uint64_t cmax = (n - 1) / N + 1;
-    const uint8_t *sb = e + 12 * (size_t)N + off;  // stream start
-    uint8_t *outb = raw + a.raw_off[b];
-    const bool vec_ok = ((((uintptr_t)outb) | N) & 15) == 0;
-    bool err = false;
-
-    // ---- fast-path lane state
-    uint32_t x = (uint32_t)X;
-    uint64_t win = 0;
-    uint32_t nbits = 0;
-    uint64_t consumed = 0;  // bits
-    const uintptr_t lo_lim = ((uintptr_t)a.enc_off[b] + (uintptr_t)enc) & ~(uintptr_t)3;
-    uintptr_t rp = 0;
-    // ---- generic lane state
-    uint64_t pos = L;
-
-    if (!GENERIC && active) {
-        const uintptr_t pend = (uintptr_t)sb + L;
-        const uintptr_t a0 = (pend - 1) & ~(uintptr_t)3;
-        const uint32_t v = (uint32_t)(pend - a0);  // 1..4 valid bytes in the first dword
-        const uint32_t w0 = *reinterpret_cast<const uint32_t *>(a0 > lo_lim ? a0 : lo_lim);
-        win = (uint64_t)(w0 << (32 - 8 * v)) << 32;
-        nbits = 8 * v;
-        rp = a0 - 4;
-    }
-
-    for (uint64_t k0 = 0; k0 < cmax; k0 += TILE) {
-        const uint32_t rows = (uint32_t)min((uint64_t)TILE, cmax - k0);
-        for (uint32_t r = 0; r < rows; r++) {
-            const uint64_t k = k0 + r;
-            uint8_t sym = 0;
-            if (k < c) {
-                if (!GENERIC) {
-                    // renormalise before decoding (rans.rs:479-485): x in [16, 2^24) needs
-                    // 0, 1 or 2 bytes: sh = 8 * (#bytes) from the leading-zero count
-                    const uint32_t sh8 = (__clz(x) & 24) - 8;
-                    const uint32_t t = __builtin_amdgcn_ubfe((uint32_t)(win >> 32), 32 - sh8, sh8);
-                    x = (x << sh8) | t;
-                    win <<= sh8;
-                    nbits -= sh8;
-                    consumed += sh8;
-                    if (nbits <= 32) {
-                        const uintptr_t ra = rp > lo_lim ? rp : lo_lim;
-                        const uint32_t ww = *reinterpret_cast<const uint32_t *>(ra);
-                        win |= (uint64_t)ww << (32 - nbits);
-                        nbits += 32;
-                        rp -= 4;
-                    }
-                    const uint32_t ent = stab[x & (TOTFREQ - 1)];
-                    x = __umul24(ent >> 20, x >> TF_SHIFT) + ((ent >> 8) & 0xFFF);
-                    sym = (uint8_t)ent;
-                } else if (!err) {
-                    while (X < RANS_L) {
-                        if (pos == 0) {  // "Insufficient data for decoding" (rans.rs:480-482)
-                            err = true;
-                            break;
-                        }
-                        pos--;
-                        X = (X << 8) | sb[pos];
-                    }
-                    if (!err) {
-                        const uint32_t slot = (uint32_t)(X & (TOTFREQ - 1));
-                        const uint32_t sy = stab[slot] & 0xFF;
-                        X = (uint64_t)gfreq[sy] * (X >> TF_SHIFT) + slot - gstart[sy];
-                        sym = (uint8_t)sy;
-                    }
-                }
-            }
-            tile[r * 256 + threadIdx.x] = sym;
-        }
-        __syncthreads();
-        flush_tile(tile, outb, n, N, blk, k0, rows, vec_ok);
-        __syncthreads();
-    }
-    if (!GENERIC && active && consumed > 8ull * L) err = true;
-    if (err) a.status[b] = ZR_INVALID_INPUT;
 }
 
 // ----------------------------------------------------------------------
@@ -1214,12 +1096,35 @@ __global__ __launch_bounds__(256) void k_dec_xn(const uint8_t *enc, uint8_t *raw
 //     the ring two tile boundaries later, so loads have 2*DT2 steps to land.
 //     The wave waits with an exact vmcnt (stores and loads in between).
 //   * a lane whose reads outrun its ring (more than ~1.3 bytes per symbol
-//     sustained, only possible for data far from its table) sets the
-//     workgroup's redo flags: k_dec_xn<true> decodes those streams again.
+//     sustained, only possible for data far from its table) decodes its
+//     stream again with the generic per-lane loop (dec_lane_generic), as do
+//     all lanes of a workgroup holding a state outside [2^16, 2^24) or a
+//     table that is not DT_NORMAL.
 //   * output: step k of stream s is raw[k*N + s]: per step one buffer byte
 //     store per wave, row offset in an SGPR, no VALU address work.
 // ----------------------------------------------------------------------
 constexpr int RR = 32;   // ring rows (dwords) per lane
+constexpr uint32_t SCAN_FUSE = 64;  // block counts up to which the decoder scans block sums itself
+
+// One lane decodes stream s generically (decode_symbol, rans.rs:472-507: u64
+// state, byte-wise renormalisation, any table kind): the fast decoder's fallback.
+// Returns false on "Insufficient data for decoding" (rans.rs:480-482).
+__device__ __noinline__ bool dec_lane_generic(const RansDTab *T, const uint32_t *lds_slot, const uint8_t *sb,
+                                              uint32_t L, uint64_t X, uint64_t c, uint8_t *obuf, uint32_t N,
+                                              uint32_t s) {
+    uint64_t pos = L;
+    for (uint64_t k = 0; k < c; k++) {
+        while (X < RANS_L) {
+            if (pos == 0) return false;
+            X = (X << 8) | sb[--pos];
+        }
+        const uint32_t slot = (uint32_t)(X & (TOTFREQ - 1));
+        const uint32_t sy = lds_slot[slot] & 0xFF;
+        X = (uint64_t)T->freq[sy] * (X >> TF_SHIFT) + slot - T->start[sy];
+        obuf[k * N + s] = (uint8_t)sy;
+    }
+    return true;
+}
 constexpr int DT2 = 16;  // steps per tile
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
@@ -1248,6 +1153,25 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
     if (n == 0 || single_mode(n, N) || a.status[b] != 0) return;
+    // the buffer's scan of block length sums (k_scan, fused for nblk <= SCAN_FUSE
+    // blocks: every wave sums the <= 64 block sums itself) and its check
+    // "Invalid stream data length" (rans.rs:608-610), before any stream read
+    const uint32_t nblk = w.nblk;
+    uint64_t blo;
+    {
+        const uint32_t blk0 = (blockIdx.x % nblkF) * FW / 256;
+        if (nblk <= SCAN_FUSE) {
+            const uint32_t l = threadIdx.x & 63;
+            const uint64_t v = l < nblk ? w.blocksum[(size_t)b * nblk + l] : 0;
+            blo = wave_sum(l < blk0 ? v : 0);
+            if ((uint64_t)N * 12 + wave_sum(v) > a.enc_len[b]) {  // workgroup-uniform
+                if (threadIdx.x == 0) a.status[b] = ZR_INVALID_INPUT;
+                return;
+            }
+        } else {
+            blo = w.blockoff[(size_t)b * nblk + blk0];
+        }
+    }
     __shared__ __attribute__((aligned(16))) uint32_t lds[TOTFREQ + (RR + 1) * FW];
     uint32_t *ring = lds + TOTFREQ;
     // scan scratch and flag alias the ring (used before it is filled)
@@ -1272,7 +1196,6 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     __syncthreads();
     unsigned long long base = 0;
     for (int i = 0; i < wv; i++) base += sh[i];
-    const uint32_t nblk = w.nblk;
     // offset: the 256-stream block's scanned offset, plus (FW < 256) the
     // lengths of the block's streams below this workgroup
     const uint32_t blk0 = (blkF * FW) / 256, below = (blkF * FW) % 256;
@@ -1282,23 +1205,28 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         for (uint32_t i = tid; i < below; i += FW) v += ld_u32_u(e + 8 * (size_t)N + 4 * ((size_t)blk0 * 256 + i));
         sub = wave_sum(v);  // FW < 256 is one wave
     }
-    const uint64_t off = base + inc - L + w.blockoff[(size_t)b * nblk + blk0] + sub;
+    const uint64_t off = base + inc - L + blo + sub;
     const uint64_t X = active ? ld_u64_u(e + 8 * (size_t)s) : RANS_L;
     const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24);
     if (!fast) atomicOr(flag, 1u);
     __syncthreads();
     const uint32_t any_slow = *flag;
     __syncthreads();  // scan/flag reads complete before the ring is written
-    auto mark_redo = [&]() {  // the 256-stream blocks this workgroup covers
-        for (uint32_t i = blk0; i <= (blkF * FW + FW - 1) / 256 && i < nblk; i++) w.redo[(size_t)b * nblk + i] = 1;
-    };
-    if (any_slow) {
-        if (tid == 0) mark_redo();
-        return;
-    }
     const uint64_t c = active ? (n - s - 1) / N + 1 : 0;
     const uint64_t cmax = (n - 1) / N + 1;
     const uintptr_t sb = (uintptr_t)e + 12 * (size_t)N + off;
+    uint8_t *const obuf = raw + a.raw_off[b];
+    // the generic per-lane decoder (u64 state, any table): a table that is not
+    // DT_NORMAL or a state outside [2^16, 2^24) anywhere in the workgroup, and
+    // below, a lane whose reads outran its ring
+    auto generic = [&]() {
+        if (!dec_lane_generic(T, lds, reinterpret_cast<const uint8_t *>(sb), L, X, c, obuf, N, s))
+            a.status[b] = ZR_INVALID_INPUT;
+    };
+    if (any_slow) {
+        if (active) generic();
+        return;
+    }
     const uintptr_t pend = sb + L;
     const uintptr_t lo_lim = ((uintptr_t)e) & ~(uintptr_t)63;
     auto clampa = [&](uintptr_t p) -> uintptr_t { return p > lo_lim ? p : lo_lim; };
@@ -1468,7 +1396,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         }
         if (active) {
             if (bad) {
-                mark_redo();
+                generic();
             } else {
                 // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
                 const uint32_t consumed = (((uint32_t)pend << 3) - pos_snap) >> 3;
@@ -1482,7 +1410,9 @@ __global__ __launch_bounds__(64) void k_dec_x1_generic(const uint8_t *enc, uint8
     const uint32_t b = blockIdx.x * 64 + threadIdx.x;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
-    if (n == 0 || !single_mode(n, a.N)) return;
+    if (!single_mode(n, a.N)) return;
+    a.status[b] = ZR_OK;  // (x1 buffers: this kernel is the only status writer)
+    if (n == 0) return;
     const uint64_t len = a.enc_len[b];
     if (len < 8) {  // "rANS data too short" (rans.rs:524-526)
         a.status[b] = ZR_INVALID_INPUT;
@@ -1643,7 +1573,7 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
     for (uint32_t t = 0; t < nacc / 8; t++) out[nout + t] = (uint8_t)(acc >> (8 * t));
     nout += nacc / 8;
     for (int t = 0; t < 8; t++) out[nout + t] = (uint8_t)((uint64_t)(X >> 8) >> (8 * t));
-    if (xmin == 0 && n) a.status[b] = ZR_INVALID_INPUT;  // "Symbol {} not in frequency table"
+    a.status[b] = (xmin == 0 && n) ? ZR_INVALID_INPUT : ZR_OK;  // "Symbol {} not in frequency table"
     a.enc_len[b] = nout + 8;
 }
 
@@ -1697,7 +1627,11 @@ __global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t
     const uint32_t b = blockIdx.x * X1W + tid;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
-    if (n == 0 || !single_mode(n, a.N)) return;
+    if (!single_mode(n, a.N)) return;
+    if (n == 0) {  // (x1 buffers: this kernel is the only status writer)
+        a.status[b] = ZR_OK;
+        return;
+    }
     const uint64_t len = a.enc_len[b];
     if (len < 8) {  // "rANS data too short" (rans.rs:524-526)
         a.status[b] = ZR_INVALID_INPUT;
@@ -1707,7 +1641,7 @@ __global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t
     const uint64_t X = ld_u64_u(e + len - 8);
     uint8_t *out = raw + a.raw_off[b];
     if (!normal || X < RANS_L || X >= (1ull << 24) || len >= (1ull << 31)) {
-        if (!x1_dec_generic(T, stab, normal, e, len, X, out, n)) a.status[b] = ZR_INVALID_INPUT;
+        a.status[b] = x1_dec_generic(T, stab, normal, e, len, X, out, n) ? ZR_OK : ZR_INVALID_INPUT;
         return;
     }
     const x4u *e4 = reinterpret_cast<const x4u *>(e - (((uintptr_t)e) & 15));
@@ -1811,7 +1745,7 @@ __global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t
             err = ia < iamin;
         }
     }
-    if (err) a.status[b] = ZR_INVALID_INPUT;
+    a.status[b] = err ? ZR_INVALID_INPUT : ZR_OK;
 }
 
 
@@ -1862,7 +1796,6 @@ size_t rans_workspace_bytes(uint32_t B, uint32_t N, uint64_t max_len) {
     size_t t = 0;
     t += round_up((uint64_t)B * N * 4, 256) * 2;
     t += round_up((uint64_t)B * nblk * 8, 256) * 2;
-    t += round_up((uint64_t)B * nblk * 4, 256);
     t += (size_t)B * region;
     return t + 256;
 }
@@ -1886,7 +1819,6 @@ int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t by
     w->st_len = reinterpret_cast<uint32_t *>(take((uint64_t)B * N * 4));
     w->blocksum = reinterpret_cast<uint64_t *>(take((uint64_t)B * nblk * 8));
     w->blockoff = reinterpret_cast<uint64_t *>(take((uint64_t)B * nblk * 8));
-    w->redo = reinterpret_cast<uint32_t *>(take((uint64_t)B * nblk * 4));
     w->scratch = take((uint64_t)B * w->region);
     return ZR_OK;
 }
@@ -1959,15 +1891,14 @@ int32_t zr_histogram_dev(const uint8_t *raw, const zr_rans_batch *bt, int32_t sh
     const uint64_t items = (uint64_t)nchunk * a.B;
     // shared: 5 resident 32-KiB-LDS workgroups per CU on 256 CUs, 4 waves each
     const uint64_t grid = shared ? std::min<uint64_t>(ceil_div(items, 4), 1280) : items;
-    timer_begin("histogram", (hipStream_t)stream);
     if (shared && bt->max_len <= 1024 && a.B >= 64) {  // many small buffers: blob-store records
         const uint64_t g2 = std::min<uint64_t>(ceil_div(ceil_div(a.B, 64), 4), 1280);
-        hipLaunchKernelGGL(k_hist_small, dim3((uint32_t)g2), dim3(256), 0, (hipStream_t)stream, raw, a, hist_dev);
+        launch_timed("histogram", k_hist_small, dim3((uint32_t)g2), dim3(256), 0, (hipStream_t)stream, raw, a,
+                     hist_dev);
     } else {
-        hipLaunchKernelGGL(k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a,
-                           shared, hist_dev, chunk, nchunk);
+        launch_timed("histogram", k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a,
+                     shared, hist_dev, chunk, nchunk);
     }
-    timer_end("histogram", (hipStream_t)stream);
     ZR_HIP(hipGetLastError());
     return ZR_OK;
     ZR_GUARD_END
@@ -1978,8 +1909,22 @@ int32_t zr_rans_dtab_from_hist_dev(const uint32_t *hist_dev, uint32_t n_tables, 
     ZR_GUARD_BEGIN
     clear_error();
     if (n_tables == 0) return ZR_OK;
+    if (!hist_dev || !dtabs_dev) return set_error(ZR_INVALID_INPUT, "null argument");
     hipLaunchKernelGGL(k_tab, dim3(n_tables), dim3(256), 0, (hipStream_t)stream, hist_dev,
-                       reinterpret_cast<RansDTab *>(dtabs_dev));
+                       reinterpret_cast<RansDTab *>(dtabs_dev), nullptr);
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_rans_dtab_from_hist_consume_dev(uint32_t *hist_dev, uint32_t n_tables, void *dtabs_dev,
+                                           void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (n_tables == 0) return ZR_OK;
+    if (!hist_dev || !dtabs_dev) return set_error(ZR_INVALID_INPUT, "null argument");
+    hipLaunchKernelGGL(k_tab, dim3(n_tables), dim3(256), 0, (hipStream_t)stream, hist_dev,
+                       reinterpret_cast<RansDTab *>(dtabs_dev), hist_dev);
     ZR_HIP(hipGetLastError());
     return ZR_OK;
     ZR_GUARD_END
@@ -1998,13 +1943,13 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
     int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
     if (st) return st;
     hipStream_t s = (hipStream_t)stream;
-    ZR_HIP(hipMemsetAsync(bt->status, 0, sizeof(int32_t) * a.B, s));
+    // (no status memset: every buffer's status has exactly one writer per call,
+    // the compaction for xN buffers and the x1 encoder for the others)
     const uint64_t gx = (uint64_t)w.nblk * a.B;
     if (bt->max_len >= a.N && a.N > 1) {
         const bool narrow = narrow_batch(a);
         if (narrow)  // the narrow encoder adds wave sums into the block sums
             ZR_HIP(hipMemsetAsync(w.blocksum, 0, sizeof(uint64_t) * gx, s));
-        timer_begin("rans_encode", s);
 #ifdef ZR_DIAG
         static const int ablate = getenv("ZR_ABLATE") ? atoi(getenv("ZR_ABLATE")) : 0;
         auto kenc = ablate == 1 ? k_enc_xn<256, 1> : ablate == 2 ? k_enc_xn<256, 2> : ablate == 3 ? k_enc_xn<256, 3>
@@ -2013,29 +1958,29 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         auto kenc = k_enc_xn<256, 0>;
 #endif
         if (narrow)
-            hipLaunchKernelGGL((k_enc_xn<64, 0>), dim3((uint32_t)(ceil_div(a.N, 64) * a.B)), dim3(64), 0, s, raw, a, w);
+            launch_timed("rans_encode", k_enc_xn<64, 0>, dim3((uint32_t)(ceil_div(a.N, 64) * a.B)), dim3(64), 0, s,
+                         raw, a, w);
         else
-            hipLaunchKernelGGL(kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
-        timer_end("rans_encode", s);
-        timer_begin("rans_compact", s);
+            launch_timed("rans_encode", kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
 #ifdef ZR_DIAG
         static const int cmp_old = getenv("ZR_COMPACT_OLD") ? 1 : 0;  // A/B diagnostics
         if (cmp_old) {
             hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
-            hipLaunchKernelGGL(k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
+            launch_timed("rans_compact", k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
         } else
 #endif
-        // 16 streams per group, 19 KiB windows (8 workgroups per CU), four 16-B loads in
-        // flight per lane (A/B: 0.140 -> 0.132 ms over two); block-sum scan fused in.
-        // Window workgroups per group: half the windows the group's largest
-        // possible span needs (the typical span of incompressible data), at
-        // least one; each loops over its windows
-        constexpr uint32_t CWIN = 19 * 1024;
-        const uint64_t max_span = 16ull * w.cap + 16;
-        const uint32_t nwin = (uint32_t)std::max<uint64_t>(1, max_span / CWIN / 2);
-        hipLaunchKernelGGL((k_enc_compact_lds<16, CWIN, 4>), dim3((uint32_t)(gx * 16 * nwin)), dim3(256), 0, s, enc,
-                           a, w, nwin);
-        timer_end("rans_compact", s);
+        {
+            // 16 streams per group, 19 KiB windows (8 workgroups per CU), four 16-B loads in
+            // flight per lane (A/B: 0.140 -> 0.132 ms over two); block-sum scan fused in.
+            // Window workgroups per group: half the windows the group's largest
+            // possible span needs (the typical span of incompressible data), at
+            // least one; each loops over its windows
+            constexpr uint32_t CWIN = 19 * 1024;
+            const uint64_t max_span = 16ull * w.cap + 16;
+            const uint32_t nwin = (uint32_t)std::max<uint64_t>(1, max_span / CWIN / 2);
+            launch_timed("rans_compact", k_enc_compact_lds<16, CWIN, 4>, dim3((uint32_t)(gx * 16 * nwin)),
+                         dim3(256), 0, s, enc, a, w, nwin);
+        }
     }
     timer_begin("rans_encode_x1", s);
     if (!(bt->min_len >= a.N && a.N > 1)) {  // some buffer may take the x1 layout
@@ -2065,15 +2010,17 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
     int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
     if (st) return st;
     hipStream_t s = (hipStream_t)stream;
-    ZR_HIP(hipMemsetAsync(bt->status, 0, sizeof(int32_t) * a.B, s));
+    // (no status memset: k_dec_hdr writes the status of xN buffers first, later
+    // kernels only ever set ZR_INVALID_INPUT; the x1 decoder writes the others)
     const uint64_t gx = (uint64_t)w.nblk * a.B;
     if (bt->max_len >= a.N && a.N > 1) {
         hipLaunchKernelGGL(k_dec_hdr, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
-        hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
-        timer_begin("rans_decode", s);
+        if (w.nblk > SCAN_FUSE)  // (otherwise the decoder scans the block sums itself)
+            hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
         if (narrow_batch(a)) {
             const uint32_t nblkF = (uint32_t)ceil_div(a.N, 64);
-            hipLaunchKernelGGL((k_dec_xn_fast<64, 0>), dim3(nblkF * a.B), dim3(64), 0, s, enc, raw, a, w, nblkF);
+            launch_timed("rans_decode", k_dec_xn_fast<64, 0>, dim3(nblkF * a.B), dim3(64), 0, s, enc, raw, a, w,
+                         nblkF);
         } else {
             const uint32_t nblkF = (uint32_t)ceil_div(a.N, 1024);
 #ifdef ZR_DIAG
@@ -2090,10 +2037,8 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
 #else
             auto kern = k_dec_xn_fast<1024, 0>;
 #endif
-            hipLaunchKernelGGL(kern, dim3(nblkF * a.B), dim3(1024), 0, s, enc, raw, a, w, nblkF);
+            launch_timed("rans_decode", kern, dim3(nblkF * a.B), dim3(1024), 0, s, enc, raw, a, w, nblkF);
         }
-        timer_end("rans_decode", s);
-        hipLaunchKernelGGL(k_dec_xn<true>, dim3((uint32_t)gx), dim3(256), 0, s, enc, raw, a, w);
     }
     timer_begin("rans_decode_x1", s);
     if (!(bt->min_len >= a.N && a.N > 1)) {

@@ -78,14 +78,19 @@ class RansDeviceBatch:
         return torch.zeros(max(1, self.enc_bytes), dtype=torch.uint8, device=self.device)
 
     # ---- pipeline stages
-    def histogram(self, raw, stream=None):
-        check(self.L.zr_memset_dev(_ptr(self.hist), 0, self.hist.numel() * 4, _stream(stream)))
+    def histogram(self, raw, stream=None, zeroed=False):
+        """Count raw's bytes into self.hist. zeroed=True: the caller knows hist is
+        all zero (fresh, or after tables_from_hist(consume=True)), so no memset."""
+        if not zeroed:
+            check(self.L.zr_memset_dev(_ptr(self.hist), 0, self.hist.numel() * 4, _stream(stream)))
         check(self.L.zr_histogram_dev(_ptr(raw), ctypes.byref(self.cbatch), int(self.shared),
                                       _ptr(self.hist), _stream(stream)))
 
-    def tables_from_hist(self, stream=None):
-        check(self.L.zr_rans_dtab_from_hist_dev(_ptr(self.hist), self.n_tables, _ptr(self.tables),
-                                                _stream(stream)))
+    def tables_from_hist(self, stream=None, consume=False):
+        """Rans64Encoder::new per histogram, on device. consume=True also zeroes
+        hist once read (the next histogram(zeroed=True) accumulates from zero)."""
+        fn = self.L.zr_rans_dtab_from_hist_consume_dev if consume else self.L.zr_rans_dtab_from_hist_dev
+        check(fn(_ptr(self.hist), self.n_tables, _ptr(self.tables), _stream(stream)))
 
     def upload_tables(self, host_tables):
         arr = (_lib.RansTable * len(host_tables))(*host_tables)
