@@ -586,8 +586,8 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         tile_sync();
         *reinterpret_cast<v4u *>(&itile[lr * EW + lp]) = pend;
         tile_sync();
-        if (body_ok && t >= 2)
-            pend = *reinterpret_cast<const v4u *>(inb + ((t - 1) * ETILE + lr) * N + col);
+        if (body_ok && t >= 2)  // (non-temporal: same-box A/B 0.244 -> 0.238 ms)
+            pend = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(inb + ((t - 1) * ETILE + lr) * N + col));
         else if (t > 0)
             pend = issue_piece(t - 1);
         flush64();
@@ -1042,7 +1042,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             const uint64_t q0 = win + 16 * (uint64_t)u;  // image offset of the unit
             uint8_t *dst = reinterpret_cast<uint8_t *>(ua0 + q0);
             if (q0 >= lo && q0 + 16 <= span) {
-                *reinterpret_cast<v4u *>(dst) = *reinterpret_cast<const v4u *>(img + 16 * u);
+                // non-temporal: the encoded streams do not linger dirty in the XCD L2s
+                // (same-box A/B: the decode that reads them 0.200 -> 0.180 ms, the
+                // compaction itself unchanged)
+                __builtin_nontemporal_store(*reinterpret_cast<const v4u *>(img + 16 * u), reinterpret_cast<v4u *>(dst));
             } else {
                 for (uint32_t t = 0; t < 16; t++)
                     if (q0 + t >= lo && q0 + t < span) dst[t] = img[16 * u + t];
