@@ -175,6 +175,33 @@ def test_rans_generic_fallback_lanes(zr, oracle, nzero):
         assert bt.raw_of(out, b) == d, f"buffer {b}"
 
 
+@pytest.mark.parametrize("B", [3, 4])
+def test_rans_many_blocks_separate_scan(zr, oracle, B):
+    """More than SCAN_FUSE (64) 256-stream blocks per buffer (N = 20000): the
+    block-sum scan runs as its own kernel before the compaction and the decoder
+    (k_scan), in one-wave (B = 3) and 1024-lane (B = 4) workgroup shapes."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    N = 20000
+    lens = [5 * N + 7, 3 * N, N + 1, 7 * N + 11][:B]
+    datas = [zr.synth("u" if b % 2 else "t", n, seed=31 + b) for b, n in enumerate(lens)]
+    bt = RansDeviceBatch(lens, N)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    for b, d in enumerate(datas):
+        t = oracle.rans_table(oracle.histogram(d))
+        assert bt.encoded(enc, b) == oracle.rans_encode(t, N, d), f"buffer {b}"
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    for b, d in enumerate(datas):
+        assert bt.raw_of(out, b) == d
+
+
 def _dtab_words(bt, k=0):
     w = bt.tables.cpu().numpy().view(np.uint32)
     per = bt.tables.numel() // 4 // bt.n_tables

@@ -405,7 +405,16 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     uint4 *et = reinterpret_cast<uint4 *>(lds + RING_BYTES);
     uint8_t *itile = lds + RING_BYTES + 256 * 16;
     const uint32_t nblkE = (a.N + EW - 1) / EW;
-    const uint32_t b = blockIdx.x / nblkE, blk = blockIdx.x % nblkE;
+    // one-wave workgroups: the two 64-column halves of each 128-B input line go
+    // to workgroups on the same XCD (workgroups are dealt to the 8 XCDs round
+    // robin), so the line is fetched into one L2 once, not into two (the grid is
+    // padded to a multiple of 16)
+    uint32_t lin = blockIdx.x;
+    if (EW == 64) {
+        const uint32_t g = blockIdx.x / 16, r = blockIdx.x % 16;
+        lin = 2 * (g * 8 + (r % 8)) + r / 8;
+    }
+    const uint32_t b = lin / nblkE, blk = lin % nblkE;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
@@ -685,6 +694,10 @@ __global__ __launch_bounds__(64) void k_enc_x1_generic(const uint8_t *raw, KArgs
     a.enc_len[b] = no + 8;
 }
 
+// Block counts (256-stream blocks per buffer) up to which the compaction and the
+// decoder scan the block sums themselves; above, k_scan runs first.
+constexpr uint32_t SCAN_FUSE = 64;
+
 // per-buffer exclusive scan of block sums; validates decode headers
 __global__ __launch_bounds__(256) void k_scan(KArgs a, RansWork w, int decode) {
     const uint32_t b = blockIdx.x;
@@ -879,25 +892,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
     // the buffer's scan of block byte sums (k_scan, fused): this block's
     // offset, and for group 0 the encoded length and the final status
-    uint64_t below = 0, all = 0, flagged = 0;
-    for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
-        const uint64_t v = w.blocksum[(size_t)b * nblk + i];
-        const uint64_t c = v & ~BS_ERR;
-        below += i < blk ? c : 0;
-        all += c;
-        flagged |= v >> 63;
-    }
-    // one reduction: the bytes below this block (< 2^55), and above them the
-    // number of threads that saw a block flagged by k_enc_xn
-    const uint64_t r = block_sum(below | (flagged << 55), sh);
-    const uint64_t bo = r & ((1ull << 55) - 1);
-    const bool failed = (r >> 55) != 0;
-    if (grp == 0 && wi == 0) {  // workgroup-uniform: the buffer's status and length
-        const uint64_t tot = block_sum(all, sh);
-        if (threadIdx.x == 0) {
-            a.enc_len[b] = (uint64_t)N * 12 + tot;
-            a.status[b] = failed ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an xN encode
+    // (more than SCAN_FUSE blocks: k_scan ran first and wrote the offsets, the
+    // encoded length and the status)
+    uint64_t bo;
+    bool failed;
+    if (nblk <= SCAN_FUSE) {
+        uint64_t below = 0, all = 0, flagged = 0;
+        for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
+            const uint64_t v = w.blocksum[(size_t)b * nblk + i];
+            const uint64_t c = v & ~BS_ERR;
+            below += i < blk ? c : 0;
+            all += c;
+            flagged |= v >> 63;
         }
+        // one reduction: the bytes below this block (< 2^55), and above them the
+        // number of threads that saw a block flagged by k_enc_xn
+        const uint64_t r = block_sum(below | (flagged << 55), sh);
+        bo = r & ((1ull << 55) - 1);
+        failed = (r >> 55) != 0;
+        if (grp == 0 && wi == 0) {  // workgroup-uniform: the buffer's status and length
+            const uint64_t tot = block_sum(all, sh);
+            if (threadIdx.x == 0) {
+                a.enc_len[b] = (uint64_t)N * 12 + tot;
+                a.status[b] = failed ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an xN encode
+            }
+        }
+    } else {
+        bo = w.blockoff[(size_t)b * nblk + blk];
+        failed = a.status[b] != 0;
     }
     if (failed) return;
     const uint32_t tid = threadIdx.x;
@@ -1107,7 +1129,6 @@ __global__ __launch_bounds__(256) void k_dec_hdr(const uint8_t *enc, KArgs a, Ra
 //     store per wave, row offset in an SGPR, no VALU address work.
 // ----------------------------------------------------------------------
 constexpr int RR = 32;   // ring rows (dwords) per lane
-constexpr uint32_t SCAN_FUSE = 64;  // block counts up to which the decoder scans block sums itself
 
 // One lane decodes stream s generically (decode_symbol, rans.rs:472-507: u64
 // state, byte-wise renormalisation, any table kind): the fast decoder's fallback.
@@ -1961,7 +1982,7 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         auto kenc = k_enc_xn<256, 0>;
 #endif
         if (narrow)
-            launch_timed("rans_encode", k_enc_xn<64, 0>, dim3((uint32_t)(ceil_div(a.N, 64) * a.B)), dim3(64), 0, s,
+            launch_timed("rans_encode", k_enc_xn<64, 0>, dim3((uint32_t)round_up(ceil_div(a.N, 64) * a.B, 16)), dim3(64), 0, s,
                          raw, a, w);
         else
             launch_timed("rans_encode", kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
@@ -1973,6 +1994,8 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         } else
 #endif
         {
+            if (w.nblk > SCAN_FUSE)  // (otherwise the compaction scans the block sums itself)
+                hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
             // 16 streams per group, 19 KiB windows (8 workgroups per CU), four 16-B loads in
             // flight per lane (A/B: 0.140 -> 0.132 ms over two); block-sum scan fused in.
             // Window workgroups per group: half the windows the group's largest
