@@ -2,9 +2,11 @@
 # Round GPU check: gpu tests, smoke, all bench workloads (logs under gpurun_out/).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gputests.log 2>&1 && \
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > gpurun_out/gputests.log 2>&1 && \
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_rans.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --buffers 1 --buffer-mib 256 --steps 4 > gpurun_out/bench_lit.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --workload fse > gpurun_out/bench_fse.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --workload o1 > gpurun_out/bench_o1.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --workload blob > gpurun_out/bench_blob.log 2>&1 && \
