@@ -27,5 +27,9 @@ from .fse import (EntropyStats, FseConfig, FseDecoder, FseDevice, FseEncoder,  #
 from .huffman import (ContextualHuffmanDecoder, ContextualHuffmanEncoder, HuffmanCompressor,  # noqa: F401,E402
                       HuffmanDecoder, HuffmanEncoder, HuffmanO1Device, HuffmanOrder, HuffmanTree, InterleavingFactor)
 from .compression import RansCompressor  # noqa: F401,E402
+# the src/entropy/mod.rs facade (EntropyAlgorithm there is zipora_amd.entropy.EntropyAlgorithm;
+# the top-level name is dict_zip's, as in the reference's pa-zip stage)
+from . import entropy  # noqa: F401,E402
+from .entropy import EntropyConfig  # noqa: F401,E402
 from .pazip import (DictZipEntropyStage, EntropyAlgorithm, PaZipFseConfig,  # noqa: F401,E402
                     apply_fse_compression, remove_fse_compression)

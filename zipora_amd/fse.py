@@ -79,14 +79,9 @@ class FseConfig:
         return c
 
 
-@dataclass
-class EntropyStats:
-    input_size: int = 0
-    output_size: int = 0
-
-    @property
-    def compression_ratio(self):
-        return self.output_size / self.input_size if self.input_size else 0.0
+# the facade's EntropyStats (mod.rs:241-330); the FSE coders record sizes only
+# (entropy 0.0: a float diagnostic off the hot path)
+from .entropy import EntropyStats  # noqa: E402
 
 
 def _u8(data):
