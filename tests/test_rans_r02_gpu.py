@@ -175,6 +175,31 @@ def test_rans_generic_fallback_lanes(zr, oracle, nzero):
         assert bt.raw_of(out, b) == d, f"buffer {b}"
 
 
+def test_rans_narrow_many_workgroups(zr, oracle):
+    """One-wave workgroups beyond three per CU (N = 64, 900 buffers: 900
+    workgroups): the decoder keeps its 4-byte slot entries there."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    N, B = 64, 900
+    rnd = random.Random(17)
+    lens = [rnd.randrange(N, 3000) for _ in range(B)]
+    datas = [zr.synth("t", n, seed=400 + b) for b, n in enumerate(lens)]
+    bt = RansDeviceBatch(lens, N, shared_table=True)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    t = oracle.rans_table(oracle.histogram(b"".join(datas)))
+    for b in range(0, B, 97):
+        assert bt.encoded(enc, b) == oracle.rans_encode(t, N, datas[b]), f"buffer {b}"
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    assert torch.equal(out, raw)
+
+
 @pytest.mark.parametrize("B", [3, 4])
 def test_rans_many_blocks_separate_scan(zr, oracle, B):
     """More than SCAN_FUSE (64) 256-stream blocks per buffer (N = 20000): the

@@ -20,6 +20,7 @@ namespace zr {
 
 // ------------------------------------------------------------------ helpers
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t ld_u32_u(const uint8_t *p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
@@ -1167,7 +1168,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
 // ABL: diagnostic ablations for profiling only, ZR_DIAG builds (1: no output
 // stores, 2: no slot table read, 4: no ring refills, 8: per-workgroup timeline
 // records written to the workspace scratch area); the product instantiates ABL = 0.
-template <int FW, int ABL>
+template <int FW, int ABL, bool WT = false>
 __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
                                                uint32_t nblkF) {
     const uint32_t b = blockIdx.x / nblkF, blkF = blockIdx.x % nblkF;
@@ -1196,8 +1197,13 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             blo = w.blockoff[(size_t)b * nblk + blk0];
         }
     }
-    __shared__ __attribute__((aligned(16))) uint32_t lds[TOTFREQ + (RR + 1) * FW];
-    uint32_t *ring = lds + TOTFREQ;
+    // slot table: 4-byte entries (sym | (slot - start) << 8 | f << 20). WT (the
+    // one-wave shape when at most 3 workgroups share a CU: LDS to spare) keeps
+    // 8-byte entries instead, {f | sym << 24, slot - start}, so the update is one
+    // mad_u24 straight on the entry
+    constexpr uint32_t TABW = (WT ? 2 : 1) * TOTFREQ;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[TABW + (RR + 1) * FW];
+    uint32_t *ring = lds + TABW;
     // scan scratch and flag alias the ring (used before it is filled)
     unsigned long long *sh = reinterpret_cast<unsigned long long *>(ring);
     uint32_t *flag = ring + 64;
@@ -1206,7 +1212,17 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     {
         const v4u *src = reinterpret_cast<const v4u *>(T->slot);
         v4u *dst = reinterpret_cast<v4u *>(lds);
-        for (uint32_t j = tid; j < TOTFREQ / 4; j += FW) dst[j] = src[j];
+        if (WT) {
+            for (uint32_t j = tid; j < TOTFREQ / 4; j += FW) {
+                const v4u q = src[j];
+                auto wide = [](uint32_t e) -> v2u { return v2u{(e >> 20) | (e << 24), (e >> 8) & 0xFFF}; };
+                const v2u w0 = wide(q.x), w1 = wide(q.y), w2 = wide(q.z), w3 = wide(q.w);
+                dst[2 * j] = v4u{w0.x, w0.y, w1.x, w1.y};
+                dst[2 * j + 1] = v4u{w2.x, w2.y, w3.x, w3.y};
+            }
+        } else {
+            for (uint32_t j = tid; j < TOTFREQ / 4; j += FW) dst[j] = src[j];
+        }
     }
     const uint32_t kind = T->kind;
     const uint32_t s = blkF * FW + tid;
@@ -1244,7 +1260,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // DT_NORMAL or a state outside [2^16, 2^24) anywhere in the workgroup, and
     // below, a lane whose reads outran its ring
     auto generic = [&]() {
-        if (!dec_lane_generic(T, lds, reinterpret_cast<const uint8_t *>(sb), L, X, c, obuf, N, s))
+        if (!dec_lane_generic(T, T->slot, reinterpret_cast<const uint8_t *>(sb), L, X, c, obuf, N, s))
             a.status[b] = ZR_INVALID_INPUT;
     };
     if (any_slow) {
@@ -1293,6 +1309,11 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         const uint64_t t = ((((uint64_t)x) << 32) | D) << sft;
         hi = (uint32_t)(t >> 32);
         lo = (uint32_t)t;
+        if (WT && !(ABL & 2)) {  // 8-byte entry: x = f * (x >> 12) + (slot - start), sym in the top byte
+            const v2u e2 = *reinterpret_cast<const v2u *>(reinterpret_cast<const char *>(lds) + ((hi >> 5) & 0x7FF8));
+            x = __umul24(e2.x, hi >> 20) + e2.y;
+            return e2.x >> 24;
+        }
         const uint32_t ent = (ABL & 2) ? (hi & 0x0FFFFF00u) | 0x01000000u
                                        : *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) +
                                                                              ((hi >> 6) & 0x3FFC));
@@ -2045,8 +2066,13 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
             hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
         if (narrow_batch(a)) {
             const uint32_t nblkF = (uint32_t)ceil_div(a.N, 64);
-            launch_timed("rans_decode", k_dec_xn_fast<64, 0>, dim3(nblkF * a.B), dim3(64), 0, s, enc, raw, a, w,
-                         nblkF);
+            // (8-byte slot entries while the workgroups fit three per CU)
+            if ((uint64_t)nblkF * a.B <= 3 * 256)
+                launch_timed("rans_decode", k_dec_xn_fast<64, 0, true>, dim3(nblkF * a.B), dim3(64), 0, s, enc, raw, a,
+                             w, nblkF);
+            else
+                launch_timed("rans_decode", k_dec_xn_fast<64, 0, false>, dim3(nblkF * a.B), dim3(64), 0, s, enc, raw,
+                             a, w, nblkF);
         } else {
             const uint32_t nblkF = (uint32_t)ceil_div(a.N, 1024);
 #ifdef ZR_DIAG
