@@ -358,6 +358,11 @@ __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tab
 __device__ __forceinline__ void asm_load16(v4u &dst, uintptr_t addr) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(addr) : "memory");
 }
+// the same with an immediate byte offset (no 64-bit address add per load)
+template <int OFF>
+__device__ __forceinline__ void asm_load16_off(v4u &dst, uintptr_t addr) {
+    asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF) : "memory");
+}
 
 // s_waitcnt vmcnt(min(n, 12)) with a runtime, wave-uniform n. One asm
 // statement with its own scalar branches: separate asm statements per count
@@ -1365,9 +1370,9 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         const bool issue = !(ABL & 4) && active && !pnd && (int32_t)(pos8 - lov8()) <= 64 * 8;
         const uintptr_t g = issue ? clampa(lo64 - 64) : dummy;
         asm_load16(s0, g);
-        asm_load16(s1, g + 16);
-        asm_load16(s2, g + 32);
-        asm_load16(s3, g + 48);
+        asm_load16_off<16>(s1, g);
+        asm_load16_off<32>(s2, g);
+        asm_load16_off<48>(s3, g);
         if (issue) {
             pnd = true;
             ptile = t;
