@@ -1285,7 +1285,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         p[8 * FW] = c2.x; p[9 * FW] = c2.y; p[10 * FW] = c2.z; p[11 * FW] = c2.w;
         p[12 * FW] = c3.x; p[13 * FW] = c3.y; p[14 * FW] = c3.z;
         p[15 * FW] = c3.w;                      // row 16, or the mirror row 32
-        if (r0 != 1) lring[0] = c3.w;            // row 0 itself
+        lring[((r0 + 15) & (RR - 1)) * FW] = c3.w;  // row 0 itself (r0 = 17; r0 = 1: row 16 again)
     };
     // prologue: the 64-B segment holding the last stream byte and the one below
     const uintptr_t g1 = (pend - 1) & ~(uintptr_t)63;
@@ -1298,8 +1298,17 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         put_seg((uint32_t)(g1 - 64), b0, b1, b2, b3);
     }
     // positions are tracked as byte address * 8 (mod 2^32): the ring only needs the
-    // low bits and comparisons use 32-bit differences
-    uintptr_t lo64 = g1 - 64;            // lowest resident byte (absolute)
+    // low bits and comparisons use 32-bit differences.
+    // PF (the 64-lane shape, one wave per SIMD, issue-bound): the lowest resident
+    // byte is kept as byte * 8 and as a signed offset from lo_lim (stream sets are
+    // < 2^31 bytes), so the refill address is one 32-bit max and one add, and the
+    // in-flight state is one flag per staging set. The 1024-lane shape keeps the
+    // 64-bit address and one (flag, tile) pair: measured 2.5 % faster there, the
+    // PF form 3.5 % faster at 64 lanes
+    constexpr bool PF = FW == 64;
+    uintptr_t lo64 = g1 - 64;                     // !PF: lowest resident byte
+    uint32_t lo8 = (uint32_t)(g1 - 64) << 3;      // PF: lowest resident byte * 8
+    int32_t lo = (int32_t)((g1 - 64) - lo_lim);  // PF: the same, from lo_lim (>= -64)
     uint32_t pos8 = (uint32_t)pend << 3;  // bytes [.., pos) not yet consumed
     uint32_t x = (uint32_t)X;
     // D: the 4 stream bytes below p (byte p-1 on top)
@@ -1328,7 +1337,8 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     uint32_t sink = 0;
     // staging registers of the segment loads issued at even / odd boundaries
     v4u e0 = {0, 0, 0, 0}, e1 = e0, e2 = e0, e3 = e0, o0 = e0, o1 = e0, o2 = e0, o3 = e0;
-    bool pnd = false;  // this lane has a segment in flight
+    bool pnd_e = false, pnd_o = false;  // PF: a segment in flight in the even / odd staging set
+    bool pnd = false;                   // !PF: a segment in flight, fetched at boundary ptile
     uint32_t ptile = 0;
     bool bad = false;
     const uint64_t wbase = (uint64_t)blkF * FW + (tid & ~63u);
@@ -1342,14 +1352,28 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     __amdgpu_buffer_rsrc_t orsrc = byte_rsrc(outb);
     const uint32_t voff = active ? tid : 0x80000000u;
     const uint32_t nfull = (uint32_t)((cmax - 1) / DT2);  // tiles with k0 + DT2 < cmax
-    auto lov8 = [&]() -> uint32_t { return (uint32_t)lo64 << 3; };
+    auto lov8 = [&]() -> uint32_t { return PF ? lo8 : (uint32_t)lo64 << 3; };
+    // a segment lands: the staging set becomes the 64 bytes below the resident ones
+    auto land = [&](const v4u c0, const v4u c1, const v4u c2, const v4u c3) {
+        if constexpr (PF) {
+            lo8 -= 512;
+            lo -= 64;
+            put_seg(lo8 >> 3, c0, c1, c2, c3);
+        } else {
+            lo64 -= 64;
+            put_seg((uint32_t)lo64, c0, c1, c2, c3);
+        }
+    };
+
     // lanes that fetch nothing at a boundary load a line of the table instead
-    // (L2-resident, one request per wave): the loads are issued unconditionally
-    // so that no control flow ever merges a staging register still in flight
+    // (L2-resident, one request per wave; a lane-private re-load measured 2x
+    // slower at 1024 lanes per CU): the loads are issued unconditionally so
+    // that no control flow ever merges a staging register still in flight
     const uintptr_t dummy = (uintptr_t)T->slot + 64 * (tid >> 6);
 
-    // tile boundary t, staging set (s0..s3) = the set of parity t & 1
-    auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3) {
+    // tile boundary t, staging set (s0..s3) = the set of parity t & 1, pmine its
+    // in-flight flag
+    auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3, bool &pmine, bool pother) {
         // every read of the previous tile was at or above pos - 4
         bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if (t >= 2) {
@@ -1360,20 +1384,22 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
                 asm volatile("s_waitcnt vmcnt(4)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
             else
                 asm volatile("s_waitcnt vmcnt(36)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
-            if (pnd && ptile + 2 == t) {
-                lo64 -= 64;
-                put_seg((uint32_t)lo64, s0, s1, s2, s3);
-                pnd = false;
+            if (PF ? pmine : pnd && ptile + 2 == t) {  // the segment this set fetched at boundary t - 2
+                land(s0, s1, s2, s3);
+                pmine = pnd = false;
             }
         }
         // a lane with <= 64 unread resident bytes fetches the segment below
-        const bool issue = !(ABL & 4) && active && !pnd && (int32_t)(pos8 - lov8()) <= 64 * 8;
-        const uintptr_t g = issue ? clampa(lo64 - 64) : dummy;
+        const bool issue =
+            !(ABL & 4) && active && (PF ? !pmine && !pother : !pnd) && (int32_t)(pos8 - lov8()) <= 64 * 8;
+        const uintptr_t g = !issue ? dummy : PF ? lo_lim + (uint32_t)max(lo - 64, 0) : clampa(lo64 - 64);
         asm_load16(s0, g);
         asm_load16_off<16>(s1, g);
         asm_load16_off<32>(s2, g);
         asm_load16_off<48>(s3, g);
-        if (issue) {
+        if constexpr (PF) {
+            pmine = pmine || issue;
+        } else if (issue) {
             pnd = true;
             ptile = t;
         }
@@ -1404,10 +1430,10 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
 
     if (wave_live) {
         for (uint32_t t = 0; t < nfull; t += 2) {
-            boundary(t, e0, e1, e2, e3);
+            boundary(t, e0, e1, e2, e3, pnd_e, pnd_o);
             tile(t);
             if (t + 1 < nfull) {
-                boundary(t + 1, o0, o1, o2, o3);
+                boundary(t + 1, o0, o1, o2, o3, pnd_o, pnd_e);
                 tile(t + 1);
             }
         }
@@ -1415,12 +1441,14 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
                      "+v"(o2), "+v"(o3)::"memory");
         bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
-        if (pnd) {
-            lo64 -= 64;
+        if constexpr (PF) {
+            if (pnd_o) land(o0, o1, o2, o3);
+            if (pnd_e) land(e0, e1, e2, e3);
+        } else if (pnd) {
             if (ptile & 1)
-                put_seg((uint32_t)lo64, o0, o1, o2, o3);
+                land(o0, o1, o2, o3);
             else
-                put_seg((uint32_t)lo64, e0, e1, e2, e3);
+                land(e0, e1, e2, e3);
         }
         uint32_t pos_snap = pos8;
         const uint64_t k0 = (uint64_t)nfull * DT2;
