@@ -108,6 +108,40 @@ def test_rans_narrow_shape_ragged(zr, oracle, N):
         assert bt.raw_of(out, b) == d
 
 
+@pytest.mark.parametrize("N,per,B,skew", [(100, 1208, 3, False), (100, 1209, 3, False), (100, 1208, 2, True),
+                                           (4096, 1208, 17, False), (4096, 1208, 17, True), (1000, 300, 70, True)])
+def test_rans_scratch_layouts(zr, oracle, N, per, B, skew):
+    """Both scratch layouts of the xN encoder (RansWork::il): per-stream capacity
+    2 * per + 16 = 2432 B is the largest lane-interleaved one, 2434 B the
+    smallest stream-contiguous one. Groups of 16 streams whose destination spans
+    two compaction windows, and (skew) streams of very different lengths in one
+    group: every third stream of the period-N interleave sees one constant byte."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    lens = [N * per - (b % 3) for b in range(B)]
+    datas = []
+    for b, n in enumerate(lens):
+        d = np.frombuffer(zr.synth("u", n, seed=900 + b), dtype=np.uint8).copy()
+        if skew:
+            d[(np.arange(n) % N) % 3 == 0] = 65
+        datas.append(d.tobytes())
+    bt = RansDeviceBatch(lens, N)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    for b, d in enumerate(datas):
+        t = oracle.rans_table(oracle.histogram(d))
+        assert bt.encoded(enc, b) == oracle.rans_encode(t, N, d), f"buffer {b} (n={len(d)})"
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    for b, d in enumerate(datas):
+        assert bt.raw_of(out, b) == d
+
+
 def test_status_written_without_zeroing(zr, oracle):
     """encode/decode write every buffer's status themselves (no memset in the
     call): xN and x1 buffers, an empty one, a symbol missing from its table

@@ -401,7 +401,9 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 // a ring address wraps with one AND): ring 32 dwords x EW lanes | encode table
 // 256 x 16 B | input tile 16 rows x EW bytes. EW = 256: exactly 40 KiB, four
 // workgroups (16 waves) per CU.
-template <uint32_t EW, int ABL>
+// IL: the batch's scratch layout (RansWork::il), a template parameter so that
+// the long-stream (contiguous) instance keeps its constant addressing.
+template <uint32_t EW, int ABL, bool IL>
 __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
     constexpr uint32_t ERS = 32;    // ring slots (dwords) per lane
     constexpr uint32_t ETILE = 16;  // input rows (steps) per tile
@@ -468,8 +470,14 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         }
         return v;
     };
-    uint32_t *out = reinterpret_cast<uint32_t *>(w.scratch + (size_t)b * w.region + (size_t)s * w.cap);
-    v4u *out4 = reinterpret_cast<v4u *>(out);
+    // scratch: quad q (16 B) of this stream at qbase + q * qstride (RansWork::il)
+    const uint32_t ln = tid & 63;  // = s & 63
+    uint8_t *const qbase = w.scratch + (size_t)b * w.region + (size_t)(s - ln) * w.cap + (IL ? ln * 16 : (size_t)ln * w.cap);
+    constexpr uint32_t qstride = IL ? 64 * 16 : 16;
+    auto quad = [&](uint32_t q) -> v4u * { return reinterpret_cast<v4u *>(qbase + q * qstride); };
+    auto dword = [&](uint32_t d) -> uint32_t * {
+        return reinterpret_cast<uint32_t *>(qbase + (d >> 2) * qstride + (d & 3) * 4);
+    };
     uint32_t X = RANS_L << 8;
     uint64_t acc = 0;   // pending output bits (emission order from bit 0)
     uint32_t nacc = 0;  // valid bits in acc, < 32 after every push
@@ -532,10 +540,11 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
                 for (int i = 0; i < 16; i++) d[i] = r[i * EW];
                 const uint32_t o = nfl >> 2;
                 if (!(ABL & 1)) {
-                    out4[o + 0] = v4u{d[0], d[1], d[2], d[3]};
-                    out4[o + 1] = v4u{d[4], d[5], d[6], d[7]};
-                    out4[o + 2] = v4u{d[8], d[9], d[10], d[11]};
-                    out4[o + 3] = v4u{d[12], d[13], d[14], d[15]};
+                    v4u *q0 = quad(o);
+                    *q0 = v4u{d[0], d[1], d[2], d[3]};
+                    *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + qstride) = v4u{d[4], d[5], d[6], d[7]};
+                    *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + 2 * qstride) = v4u{d[8], d[9], d[10], d[11]};
+                    *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + 3 * qstride) = v4u{d[12], d[13], d[14], d[15]};
                 } else {
                     asm volatile("" ::"v"(d[0]), "v"(d[15]));
                 }
@@ -630,13 +639,13 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     {
         const uint32_t *r = ring + tid;
         while (nw - nfl >= 4) {
-            out4[nfl >> 2] = v4u{r[(nfl & (ERS - 1)) * EW], r[((nfl + 1) & (ERS - 1)) * EW],
-                                 r[((nfl + 2) & (ERS - 1)) * EW], r[((nfl + 3) & (ERS - 1)) * EW]};
+            *quad(nfl >> 2) = v4u{r[(nfl & (ERS - 1)) * EW], r[((nfl + 1) & (ERS - 1)) * EW],
+                                  r[((nfl + 2) & (ERS - 1)) * EW], r[((nfl + 3) & (ERS - 1)) * EW]};
             nfl += 4;
         }
-        for (; nfl < nw; nfl++) out[nfl] = r[(nfl & (ERS - 1)) * EW];
+        for (; nfl < nw; nfl++) *dword(nfl) = r[(nfl & (ERS - 1)) * EW];
     }
-    if (nacc) out[nw] = (uint32_t)acc;
+    if (nacc) *dword(nw) = (uint32_t)acc;
     // "Symbol {} not in frequency table" (rans.rs:311-316): flagged in the top bit
     // of the block's byte sum (BS_ERR); the compaction turns it into the status
     const bool bad = err || xmin == 0;
@@ -736,118 +745,6 @@ __global__ __launch_bounds__(256) void k_scan(KArgs a, RansWork w, int decode) {
     }
 }
 
-#ifdef ZR_DIAG  // the previous compaction, kept for A/B runs (ZR_COMPACT_OLD=1)
-// header + stream compaction of the xN layout (rans.rs:402-419)
-constexpr uint32_t CSPLIT = 4;  // workgroups per 256-stream block (more bytes in flight per CU)
-__global__ __launch_bounds__(256) void k_enc_compact(uint8_t *enc, KArgs a, RansWork w) {
-    const uint32_t nblk = w.nblk;
-    const uint32_t part = blockIdx.x % CSPLIT;
-    const uint32_t b = blockIdx.x / CSPLIT / nblk, blk = (blockIdx.x / CSPLIT) % nblk;
-    if (b >= a.B) return;
-    const uint64_t n = a.len[b];
-    const uint32_t N = a.N;
-    if (single_mode(n, N) || a.status[b] != 0) return;
-    __shared__ unsigned long long sh[4];
-    __shared__ uint64_t soff[256];
-    __shared__ uint32_t slen[256];
-    const uint32_t s = blk * 256 + threadIdx.x;
-    const bool active = s < N;
-    const uint32_t L = active ? w.st_len[(size_t)b * N + s] : 0;
-    const uint64_t off = block_excl_scan(L, sh, nullptr) + w.blockoff[(size_t)b * nblk + blk];
-    soff[threadIdx.x] = off;
-    slen[threadIdx.x] = L;
-    uint8_t *e = enc + a.enc_off[b];
-    if (active && part == 0) {
-        const uint32_t x = w.st_state[(size_t)b * N + s];
-        st_u32_u(e + 8 * (size_t)s, x);
-        st_u32_u(e + 8 * (size_t)s + 4, 0);
-        st_u32_u(e + 8 * (size_t)N + 4 * (size_t)s, L);
-    }
-    __syncthreads();
-    // The block's 256 streams are contiguous in the destination. Each thread
-    // owns aligned 16-byte destination units (unit u = thread + 256 i) and
-    // finds the stream holding it by a forward scan of the stream offsets in
-    // LDS; interior units gather 16 source bytes with 5 dword loads +
-    // v_alignbyte, units crossing a stream boundary go byte by byte.
-    __shared__ uint64_t send_s[256];
-    send_s[threadIdx.x] = off + L;  // (exclusive end offsets, relative to the buffer's stream area)
-    __syncthreads();
-    uint8_t *dbase = e + 12 * (size_t)N;
-    const uint32_t nstream = min(256u, N - blk * 256);
-    const uint64_t r0 = soff[0], r1 = send_s[nstream - 1];  // destination range [r0, r1)
-    if (r1 > r0) {
-        const uintptr_t ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
-        const uint64_t nunits = ((uintptr_t)dbase + r1 - ua0 + 15) / 16;
-        const uint64_t ulo = nunits * part / CSPLIT, uhi = nunits * (part + 1) / CSPLIT;
-        // first stream ending after this thread's first unit: binary search (a
-        // linear scan from stream 0 costs part*64 dependent LDS reads)
-        uint32_t sj = 0;
-        {
-            const int64_t p = (int64_t)(ua0 + 16 * (ulo + threadIdx.x) - (uintptr_t)dbase);
-            uint32_t lo = 0, hi = nstream - 1;  // send_s[hi] > p or hi = last
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if ((int64_t)send_s[mid] <= p) lo = mid + 1;
-                else hi = mid;
-            }
-            sj = lo;
-        }
-        for (uint64_t u = ulo + threadIdx.x; u < uhi; u += 256) {
-            const uintptr_t ua = ua0 + 16 * u;
-            // destination offset of the unit; negative for a first unit that starts in the header
-            const int64_t p0 = (int64_t)(ua - (uintptr_t)dbase);
-            while (sj + 1 < nstream && (int64_t)send_s[sj] <= p0) sj++;
-            const int64_t o = p0 - (int64_t)soff[sj];  // source offset in stream sj
-            const uint8_t *src = w.scratch + (size_t)b * w.region + (size_t)(blk * 256 + sj) * w.cap;
-            const uint8_t *sbase = w.scratch + (size_t)b * w.region + (size_t)(blk * 256) * w.cap;
-            // 16 source bytes of stream j starting at source offset o (o may be
-            // negative: bytes before the stream are read but masked off later)
-            auto gather16 = [&](uint32_t j, int64_t o) -> uint4 {
-                const uint8_t *src = sbase + (size_t)j * w.cap;
-                const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src + (o & ~(int64_t)3));
-                const uint32_t r = (uint32_t)(o & 3) * 8;
-                const uint32_t w0 = s4[0], w1 = s4[1], w2 = s4[2], w3 = s4[3], w4 = s4[4];
-                uint4 v;
-                v.x = (uint32_t)((((uint64_t)w1 << 32) | w0) >> r);
-                v.y = (uint32_t)((((uint64_t)w2 << 32) | w1) >> r);
-                v.z = (uint32_t)((((uint64_t)w3 << 32) | w2) >> r);
-                v.w = (uint32_t)((((uint64_t)w4 << 32) | w3) >> r);
-                return v;
-            };
-            const int64_t endj = (int64_t)send_s[sj] - p0;  // unit bytes [0, endj) lie in stream sj
-            const bool inside = p0 >= (int64_t)r0 && p0 + 16 <= (int64_t)r1;
-            if (o >= 0 && endj >= 16) {
-                *reinterpret_cast<uint4 *>(ua) = gather16(sj, o);  // interior unit
-            } else if (inside && o >= 0 && sj + 1 < nstream &&
-                       ((int64_t)send_s[sj + 1] - p0 >= 16 || sj + 2 == nstream)) {
-                // unit crossing one stream boundary at byte endj: merge two gathers
-                const uint4 A = gather16(sj, o), Bv = gather16(sj + 1, -endj);
-                auto msk = [&](int i) -> uint32_t {
-                    const int64_t k = endj - 4 * i;  // bytes of dword i taken from A
-                    return k >= 4 ? 0xFFFFFFFFu : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
-                };
-                uint4 v;
-                v.x = (A.x & msk(0)) | (Bv.x & ~msk(0));
-                v.y = (A.y & msk(1)) | (Bv.y & ~msk(1));
-                v.z = (A.z & msk(2)) | (Bv.z & ~msk(2));
-                v.w = (A.w & msk(3)) | (Bv.w & ~msk(3));
-                *reinterpret_cast<uint4 *>(ua) = v;
-            } else {
-                // range edge or a unit spanning three or more streams: byte by byte
-                uint32_t sk = sj;
-                for (int t = 0; t < 16; t++) {
-                    const int64_t p = p0 + t;
-                    if (p < (int64_t)r0 || p >= (int64_t)r1) continue;
-                    while (sk + 1 < nstream && (int64_t)send_s[sk] <= p) sk++;
-                    reinterpret_cast<uint8_t *>(ua)[t] = sbase[(size_t)sk * w.cap + (p - (int64_t)soff[sk])];
-                }
-            }
-        }
-    }
-}
-
-#endif
-
 __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, RansWork w) {
     const uint32_t b = blockIdx.x;
     if (b >= a.B) return;
@@ -875,7 +772,11 @@ __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, Ra
 // writes the image out with aligned 16-B stores. Only the two edge units of a
 // group, shared with the neighbouring groups, are stored byte by byte.
 // (8 waves per SIMD: 8 workgroups of 19 KiB LDS per CU, at most 64 VGPRs)
-template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD>  // streams per group (divides 64), window bytes, loads in flight
+// IL (RansWork::il, the lane-interleaved scratch): phase 1 walks the window's
+// chunks quad-major (lane = stream of the group), so each load instruction
+// reads the group's quad q as one 256-B run; chunks outside a stream's range
+// in the window are skipped lanes.
+template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL>  // streams per group (divides 64), window bytes, loads in flight
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_lds(
     uint8_t *enc, KArgs a, RansWork w, uint32_t nwin) {
     static_assert(CS <= 64 && 64 % CS == 0, "a group's streams are lanes of one wave");
@@ -894,7 +795,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     const uint32_t ns = min(CS, N - s0);
     __shared__ unsigned long long sh[4];
     __shared__ uint64_t soff[CS];
-    __shared__ uint32_t slen[CS], cpre[CS + 1], clo[CS];
+    __shared__ uint32_t slen[CS], cpre[CS + 1], clo[CS], crng[2];
     __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
     // the buffer's scan of block byte sums (k_scan, fused): this block's
     // offset, and for group 0 the encoded length and the final status
@@ -955,6 +856,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             clo[i] = c0;
             if (i == 0) cpre[0] = 0;
         }
+        if (IL) {  // the window's quad rows [crng[0], crng[1])
+            uint32_t qa = cnt ? c0 : 0xFFFFFFFFu, qb = cnt ? c0 + cnt : 0u;
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                qa = min(qa, (uint32_t)__shfl_xor(qa, d, 64));
+                qb = max(qb, (uint32_t)__shfl_xor(qb, d, 64));
+            }
+            if (lane == 0) {
+                crng[0] = qa;
+                crng[1] = qb;
+            }
+        }
     };
     uint64_t span = 0;
     uintptr_t ua0 = 0;
@@ -1000,7 +912,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     if (r1 <= r0) return;
     ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
     span = (uintptr_t)dbase + r1 - ua0;  // bytes of the image from ua0
-    const uint8_t *sbase = w.scratch + (size_t)b * w.region + (size_t)s0 * w.cap;
+    // stream-major: stream i's chunk c at sbase + i * cap + 16 c; IL: at sbase + (64 c + i) * 16
+    const uint8_t *sbase = w.scratch + (size_t)b * w.region +
+                           (IL ? (size_t)(s0 & ~63u) * w.cap + (s0 & 63u) * 16 : (size_t)s0 * w.cap);
     const uint64_t lo = (uintptr_t)dbase + r0 - ua0;  // image bytes below lo belong to another group
     for (uint64_t win = (uint64_t)wi * CWIN; win < span; win += (uint64_t)nwin * CWIN) {
         const uint64_t wend = min(span, win + (uint64_t)CWIN);
@@ -1013,9 +927,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             }
             __syncthreads();
         }
-        const uint32_t nchunks = cpre[ns];
-        // ---- phase 1: chunks -> LDS image. Flat chunk f belongs to stream i
-        // with cpre[i] <= f < cpre[i+1].
+        // ---- phase 1: chunks -> LDS image. Stream-major: flat chunk f belongs
+        // to stream i with cpre[i] <= f < cpre[i+1]. IL: flat f is quad row
+        // crng[0] + f / CS of stream f % CS.
+        const uint32_t nchunks = IL ? (crng[1] > crng[0] ? (crng[1] - crng[0]) * CS : 0u) : cpre[ns];
+        const uint32_t qrow0 = IL ? crng[0] : 0u;
         uint32_t si = 0;
         for (uint32_t f0 = wv * 64 * CU_LD; f0 < nchunks; f0 += 256 * CU_LD) {
             v4u v[CU_LD];
@@ -1026,7 +942,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                 nv[k] = 0;
                 dpos[k] = 0;
                 const uint8_t *src = sbase;
-                if (f < nchunks) {
+                if (IL) {
+                    const uint32_t i = f % CS, c = qrow0 + f / CS;
+                    if (f < nchunks && i < ns && c - clo[i] < cpre[i + 1] - cpre[i]) {
+                        src = sbase + ((size_t)c * 64 + i) * 16;
+                        nv[k] = min(16u, slen[i] - 16 * c);
+                        dpos[k] = (int32_t)((int64_t)((uintptr_t)dbase + soff[i] - ua0) - (int64_t)win) + 16 * (int32_t)c;
+                    }
+                } else if (f < nchunks) {
                     while (cpre[si + 1] <= f) si++;
                     const uint32_t c = clo[si] + (f - cpre[si]);
                     src = sbase + (size_t)si * w.cap + 16 * (size_t)c;
@@ -1858,23 +1781,38 @@ __global__ __launch_bounds__(256) void k_rcp_selftest(unsigned long long *bad, u
 // ======================================================================
 // host launchers
 // ======================================================================
-// per-stream scratch stride: a multiple of 128 B, so the encoder's 64-byte
-// bursts fill whole halves of 128-byte lines (a 16-byte multiple left every
-// stream's bursts straddling lines)
-// (A/B on one box: 0.753 -> 0.733 ms per step; 256 measured the same as 128)
-static constexpr uint64_t scratch_align() { return 128; }
+// Scratch geometry of an xN batch (RansWork::il, cap, region). Short streams
+// (cap <= IL_MAX_CAP: a group of 16 streams spans at most two compaction
+// windows) take the lane-interleaved layout: the encoder's 64-byte bursts
+// then leave as stores whose lanes write adjacent 16-B quads (same-box A/B of
+// the encoder alone: 0.239 -> 0.201 ms), and the compaction reads 16 streams'
+// quad q as one 256-B run. Long streams keep one contiguous region per stream,
+// with a per-stream stride that is a multiple of 128 B, so the 64-byte bursts
+// fill whole halves of 128-byte lines (A/B: 0.753 -> 0.733 ms per step).
+static constexpr uint64_t IL_MAX_CAP = 2432;
+struct ScratchGeom {
+    uint64_t cap, region;
+    uint32_t il;
+};
+static ScratchGeom scratch_geom(uint32_t N, uint64_t max_len) {
+    const uint64_t cmax = ceil_div(max_len ? max_len : 1, N);
+    ScratchGeom g;
+    g.cap = round_up(2 * cmax + 16, 16);
+    g.il = g.cap <= IL_MAX_CAP;
+    if (!g.il) g.cap = round_up(g.cap, 128);
+    const uint64_t nst = g.il ? round_up(N, 64) : N;  // whole wave groups
+    g.region = std::max<uint64_t>(round_up(nst * g.cap, 256), round_up(2 * max_len + 16, 256));
+    return g;
+}
 
 size_t rans_workspace_bytes(uint32_t B, uint32_t N, uint64_t max_len) {
     if (N == 0) N = 1;
     const uint64_t nblk = ceil_div(N, 256);
-    const uint64_t cmax = ceil_div(max_len ? max_len : 1, N);
-    const uint64_t cap = round_up(2 * cmax + 16, scratch_align());
-    const uint64_t region = std::max<uint64_t>(round_up((uint64_t)N * cap, 256),
-                                               round_up(2 * max_len + 16, 256));
+    const ScratchGeom g = scratch_geom(N, max_len);
     size_t t = 0;
     t += round_up((uint64_t)B * N * 4, 256) * 2;
     t += round_up((uint64_t)B * nblk * 8, 256) * 2;
-    t += (size_t)B * region;
+    t += (size_t)B * g.region;
     return t + 256;
 }
 
@@ -1883,9 +1821,10 @@ int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t by
     if (bytes < rans_workspace_bytes(B, N, max_len))
         return set_error(ZR_INVALID_INPUT, "rANS workspace too small");
     const uint64_t nblk = ceil_div(N, 256);
-    const uint64_t cmax = ceil_div(max_len ? max_len : 1, N);
-    w->cap = (uint32_t)round_up(2 * cmax + 16, scratch_align());
-    w->region = std::max<uint64_t>(round_up((uint64_t)N * w->cap, 256), round_up(2 * max_len + 16, 256));
+    const ScratchGeom g = scratch_geom(N, max_len);
+    w->cap = (uint32_t)g.cap;
+    w->region = g.region;
+    w->il = g.il;
     w->nblk = (uint32_t)nblk;
     uint8_t *p = reinterpret_cast<uint8_t *>(round_up((uintptr_t)ws, 256));
     auto take = [&](uint64_t n) {
@@ -2030,23 +1969,18 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             ZR_HIP(hipMemsetAsync(w.blocksum, 0, sizeof(uint64_t) * gx, s));
 #ifdef ZR_DIAG
         static const int ablate = getenv("ZR_ABLATE") ? atoi(getenv("ZR_ABLATE")) : 0;
-        auto kenc = ablate == 1 ? k_enc_xn<256, 1> : ablate == 2 ? k_enc_xn<256, 2> : ablate == 3 ? k_enc_xn<256, 3>
-                                                                                            : k_enc_xn<256, 0>;
+        auto kenc = ablate == 1   ? (w.il ? k_enc_xn<256, 1, true> : k_enc_xn<256, 1, false>)
+                    : ablate == 2 ? (w.il ? k_enc_xn<256, 2, true> : k_enc_xn<256, 2, false>)
+                    : ablate == 3 ? (w.il ? k_enc_xn<256, 3, true> : k_enc_xn<256, 3, false>)
+                                  : (w.il ? k_enc_xn<256, 0, true> : k_enc_xn<256, 0, false>);
 #else
-        auto kenc = k_enc_xn<256, 0>;
+        auto kenc = w.il ? k_enc_xn<256, 0, true> : k_enc_xn<256, 0, false>;
 #endif
         if (narrow)
-            launch_timed("rans_encode", k_enc_xn<64, 0>, dim3((uint32_t)round_up(ceil_div(a.N, 64) * a.B, 16)), dim3(64), 0, s,
-                         raw, a, w);
+            launch_timed("rans_encode", w.il ? k_enc_xn<64, 0, true> : k_enc_xn<64, 0, false>,
+                         dim3((uint32_t)round_up(ceil_div(a.N, 64) * a.B, 16)), dim3(64), 0, s, raw, a, w);
         else
             launch_timed("rans_encode", kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
-#ifdef ZR_DIAG
-        static const int cmp_old = getenv("ZR_COMPACT_OLD") ? 1 : 0;  // A/B diagnostics
-        if (cmp_old) {
-            hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
-            launch_timed("rans_compact", k_enc_compact, dim3((uint32_t)gx * CSPLIT), dim3(256), 0, s, enc, a, w);
-        } else
-#endif
         {
             if (w.nblk > SCAN_FUSE)  // (otherwise the compaction scans the block sums itself)
                 hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
@@ -2058,8 +1992,8 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             constexpr uint32_t CWIN = 19 * 1024;
             const uint64_t max_span = 16ull * w.cap + 16;
             const uint32_t nwin = (uint32_t)std::max<uint64_t>(1, max_span / CWIN / 2);
-            launch_timed("rans_compact", k_enc_compact_lds<16, CWIN, 4>, dim3((uint32_t)(gx * 16 * nwin)),
-                         dim3(256), 0, s, enc, a, w, nwin);
+            launch_timed("rans_compact", w.il ? k_enc_compact_lds<16, CWIN, 4, true> : k_enc_compact_lds<16, CWIN, 4, false>,
+                         dim3((uint32_t)(gx * 16 * nwin)), dim3(256), 0, s, enc, a, w, nwin);
         }
     }
     timer_begin("rans_encode_x1", s);
