@@ -115,16 +115,25 @@ __device__ __forceinline__ void hist_range(const uint8_t *p, uint64_t lo, uint64
     const uint64_t units = (hi - body_lo) / 16;
     const v4u *q = reinterpret_cast<const v4u *>(p + body_lo);
     uint64_t u = tid;
-    // four 16-byte loads in flight per thread
-    for (; u + 3 * T < units; u += 4 * T) {
-        const v4u v0 = __builtin_nontemporal_load(q + u);
-        const v4u v1 = __builtin_nontemporal_load(q + u + T);
-        const v4u v2 = __builtin_nontemporal_load(q + u + 2 * T);
-        const v4u v3 = __builtin_nontemporal_load(q + u + 3 * T);
-        hist_add4(h, v0.x, cp); hist_add4(h, v0.y, cp); hist_add4(h, v0.z, cp); hist_add4(h, v0.w, cp);
-        hist_add4(h, v1.x, cp); hist_add4(h, v1.y, cp); hist_add4(h, v1.z, cp); hist_add4(h, v1.w, cp);
-        hist_add4(h, v2.x, cp); hist_add4(h, v2.y, cp); hist_add4(h, v2.z, cp); hist_add4(h, v2.w, cp);
-        hist_add4(h, v3.x, cp); hist_add4(h, v3.y, cp); hist_add4(h, v3.z, cp); hist_add4(h, v3.w, cp);
+    // four 16-byte loads per thread per round, the next round's issued before
+    // this round is counted (eight in flight while the LDS adds run)
+    auto add16 = [&](const v4u v) {
+        hist_add4(h, v.x, cp); hist_add4(h, v.y, cp); hist_add4(h, v.z, cp); hist_add4(h, v.w, cp);
+    };
+    if (u + 3 * T < units) {
+        v4u v0 = __builtin_nontemporal_load(q + u);
+        v4u v1 = __builtin_nontemporal_load(q + u + T);
+        v4u v2 = __builtin_nontemporal_load(q + u + 2 * T);
+        v4u v3 = __builtin_nontemporal_load(q + u + 3 * T);
+        for (u += 4 * T; u + 3 * T < units; u += 4 * T) {
+            const v4u n0 = __builtin_nontemporal_load(q + u);
+            const v4u n1 = __builtin_nontemporal_load(q + u + T);
+            const v4u n2 = __builtin_nontemporal_load(q + u + 2 * T);
+            const v4u n3 = __builtin_nontemporal_load(q + u + 3 * T);
+            add16(v0); add16(v1); add16(v2); add16(v3);
+            v0 = n0; v1 = n1; v2 = n2; v3 = n3;
+        }
+        add16(v0); add16(v1); add16(v2); add16(v3);
     }
     for (; u < units; u += T) {
         const v4u v = q[u];
@@ -796,6 +805,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     __shared__ unsigned long long sh[4];
     __shared__ uint64_t soff[CS];
     __shared__ uint32_t slen[CS], cpre[CS + 1], clo[CS], crng[2];
+    __shared__ int4 ilm[CS];  // IL, per stream in the window: quad rows [x, y), image bytes [z, w) (z: its quad 0)
     __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
     // the buffer's scan of block byte sums (k_scan, fused): this block's
     // offset, and for group 0 the encoded length and the final status
@@ -845,7 +855,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         c0 = (uint32_t)cl;
         cnt = ch > cl ? (uint32_t)(ch - cl) : 0u;
     };
-    auto publish = [&](bool mine, uint32_t i, uint32_t c0, uint32_t cnt) {  // one wave: prefix of counts
+    // one wave: prefix of counts. dbias = image position (from win) of stream i's
+    // byte 0, len its length (IL only)
+    auto publish = [&](bool mine, uint32_t i, uint32_t c0, uint32_t cnt, int32_t dbias, uint32_t len) {
         uint32_t inc = cnt;
         for (uint32_t d = 1; d < 64; d <<= 1) {
             const uint32_t t = __shfl_up(inc, d, 64);
@@ -856,7 +868,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             clo[i] = c0;
             if (i == 0) cpre[0] = 0;
         }
-        if (IL) {  // the window's quad rows [crng[0], crng[1])
+        if (IL) {  // the window's quad rows [crng[0], crng[1]); the streams' ranges
+            if (i < CS)
+                ilm[i] = mine && cnt ? make_int4((int32_t)c0, (int32_t)(c0 + cnt), dbias, dbias + (int32_t)len)
+                                     : make_int4(0, 0, 0, 0);
             uint32_t qa = cnt ? c0 : 0xFFFFFFFFu, qb = cnt ? c0 + cnt : 0u;
             for (uint32_t d = 1; d < 64; d <<= 1) {
                 qa = min(qa, (uint32_t)__shfl_xor(qa, d, 64));
@@ -905,7 +920,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         uint32_t c0 = 0, cnt = 0;
         const uint64_t win0 = (uint64_t)wi * CWIN;
         if (mine && g_r1 > g_r0) chunk_range(off, L, g_ua0, win0, min(g_span, win0 + (uint64_t)CWIN), c0, cnt);
-        if (wv == (s0 - blk * 256) / 64) publish(mine, i, c0, cnt);  // the group's wave (uniform branch)
+        const int32_t dbias = (int32_t)((int64_t)((uintptr_t)dbase + off - g_ua0) - (int64_t)win0);
+        if (wv == (s0 - blk * 256) / 64) publish(mine, i, c0, cnt, dbias, L);  // the group's wave (uniform branch)
     }
     __syncthreads();
     const uint64_t r0 = soff[0], r1 = soff[ns - 1] + slen[ns - 1];
@@ -922,8 +938,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         if (win != (uint64_t)wi * CWIN) {  // later windows (long streams): new chunk ranges
             if (tid < 64) {
                 uint32_t c0 = 0, cnt = 0;
-                if (tid < ns) chunk_range(soff[tid], slen[tid], ua0, win, wend, c0, cnt);
-                publish(tid < ns, tid, c0, cnt);
+                int32_t dbias = 0;
+                uint32_t len = 0;
+                if (tid < ns) {
+                    chunk_range(soff[tid], slen[tid], ua0, win, wend, c0, cnt);
+                    dbias = (int32_t)((int64_t)((uintptr_t)dbase + soff[tid] - ua0) - (int64_t)win);
+                    len = slen[tid];
+                }
+                publish(tid < ns, tid, c0, cnt, dbias, len);
             }
             __syncthreads();
         }
@@ -944,10 +966,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                 const uint8_t *src = sbase;
                 if (IL) {
                     const uint32_t i = f % CS, c = qrow0 + f / CS;
-                    if (f < nchunks && i < ns && c - clo[i] < cpre[i + 1] - cpre[i]) {
-                        src = sbase + ((size_t)c * 64 + i) * 16;
-                        nv[k] = min(16u, slen[i] - 16 * c);
-                        dpos[k] = (int32_t)((int64_t)((uintptr_t)dbase + soff[i] - ua0) - (int64_t)win) + 16 * (int32_t)c;
+                    if (f < nchunks) {
+                        const int4 m = ilm[i];
+                        if ((int32_t)c >= m.x && (int32_t)c < m.y) {
+                            src = sbase + (c * 64 + i) * 16;
+                            dpos[k] = m.z + 16 * (int32_t)c;
+                            nv[k] = (uint32_t)min(16, m.w - dpos[k]);
+                        }
                     }
                 } else if (f < nchunks) {
                     while (cpre[si + 1] <= f) si++;
@@ -961,7 +986,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             for (uint32_t k = 0; k < CU_LD; k++) {
                 if (!nv[k]) continue;
                 const int32_t p = dpos[k];
-                if (nv[k] == 16 && p >= 0 && p + 16 <= (int32_t)wl && (p & 3) == 0) {
+                if (IL && nv[k] == 16 && p >= 0 && p + 16 <= (int32_t)wl) {
+                    // the lanes of a row are 16 streams of different alignments
+                    // al: no per-byte loops. The chunk's bytes shifted to the
+                    // dword grid (slot j at q + 4 j): slot 0 holds 4 - al of them
+                    // (b32, or b8 + b16, b16, b8), slots 1-3 are whole, slot 4
+                    // holds al (b8, b16, or b16 + b8)
+                    const uint32_t x0 = v[k].x, x1 = v[k].y, x2 = v[k].z, x3 = v[k].w;
+                    const uint32_t al = (uint32_t)p & 3, sh = 32 - 8 * al;  // sh = 32: aligned
+                    const int32_t q = p - (int32_t)al;
+                    const uint32_t d0 = (uint32_t)(((uint64_t)x0 << 32) >> sh);
+                    const uint32_t d4 = (uint32_t)((uint64_t)x3 >> sh);
+                    uint32_t *m = reinterpret_cast<uint32_t *>(img + q + 4);
+                    m[0] = (uint32_t)((((uint64_t)x1 << 32) | x0) >> sh);
+                    m[1] = (uint32_t)((((uint64_t)x2 << 32) | x1) >> sh);
+                    m[2] = (uint32_t)((((uint64_t)x3 << 32) | x2) >> sh);
+                    if (al == 0) *reinterpret_cast<uint32_t *>(img + q) = d0;
+                    if (al & 1) img[q + al] = (uint8_t)(d0 >> (8 * al));
+                    if (al == 1 || al == 2) *reinterpret_cast<uint16_t *>(img + q + 2) = (uint16_t)(d0 >> 16);
+                    if (al >= 2) *reinterpret_cast<uint16_t *>(img + q + 16) = (uint16_t)d4;
+                    if (al & 1) img[q + 16 + (al & 2)] = (uint8_t)(d4 >> (8 * (al & 2)));
+                } else if (IL) {  // a stream's last chunk, or one across the window's edge
+                    const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                    for (uint32_t t = 0; t < nv[k]; t++) {
+                        const int32_t q = p + (int32_t)t;
+                        if (q >= 0 && q < (int32_t)wl) img[q] = (uint8_t)(wd[t >> 2] >> (8 * (t & 3)));
+                    }
+                } else if (nv[k] == 16 && p >= 0 && p + 16 <= (int32_t)wl && (p & 3) == 0) {
                     uint32_t *d = reinterpret_cast<uint32_t *>(img + p);
                     d[0] = v[k].x;
                     d[1] = v[k].y;
