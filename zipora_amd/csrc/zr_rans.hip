@@ -115,25 +115,28 @@ __device__ __forceinline__ void hist_range(const uint8_t *p, uint64_t lo, uint64
     const uint64_t units = (hi - body_lo) / 16;
     const v4u *q = reinterpret_cast<const v4u *>(p + body_lo);
     uint64_t u = tid;
-    // four 16-byte loads per thread per round, the next round's issued before
-    // this round is counted (eight in flight while the LDS adds run)
+    // HL 16-byte loads per thread per round, the next round's issued before
+    // this round is counted (2 HL in flight while the LDS adds run)
+    constexpr uint32_t HL = 8;
     auto add16 = [&](const v4u v) {
         hist_add4(h, v.x, cp); hist_add4(h, v.y, cp); hist_add4(h, v.z, cp); hist_add4(h, v.w, cp);
     };
-    if (u + 3 * T < units) {
-        v4u v0 = __builtin_nontemporal_load(q + u);
-        v4u v1 = __builtin_nontemporal_load(q + u + T);
-        v4u v2 = __builtin_nontemporal_load(q + u + 2 * T);
-        v4u v3 = __builtin_nontemporal_load(q + u + 3 * T);
-        for (u += 4 * T; u + 3 * T < units; u += 4 * T) {
-            const v4u n0 = __builtin_nontemporal_load(q + u);
-            const v4u n1 = __builtin_nontemporal_load(q + u + T);
-            const v4u n2 = __builtin_nontemporal_load(q + u + 2 * T);
-            const v4u n3 = __builtin_nontemporal_load(q + u + 3 * T);
-            add16(v0); add16(v1); add16(v2); add16(v3);
-            v0 = n0; v1 = n1; v2 = n2; v3 = n3;
+    if (u + (HL - 1) * T < units) {
+        v4u cur[HL];
+#pragma unroll
+        for (uint32_t k = 0; k < HL; k++) cur[k] = __builtin_nontemporal_load(q + u + k * T);
+        for (u += HL * T; u + (HL - 1) * T < units; u += HL * T) {
+            v4u nxt[HL];
+#pragma unroll
+            for (uint32_t k = 0; k < HL; k++) nxt[k] = __builtin_nontemporal_load(q + u + k * T);
+#pragma unroll
+            for (uint32_t k = 0; k < HL; k++) {
+                add16(cur[k]);
+                cur[k] = nxt[k];
+            }
         }
-        add16(v0); add16(v1); add16(v2); add16(v3);
+#pragma unroll
+        for (uint32_t k = 0; k < HL; k++) add16(cur[k]);
     }
     for (; u < units; u += T) {
         const v4u v = q[u];
