@@ -860,12 +860,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     };
     // one wave: prefix of counts. dbias = image position (from win) of stream i's
     // byte 0, len its length (IL only)
-    auto publish = [&](bool mine, uint32_t i, uint32_t c0, uint32_t cnt, int32_t dbias, uint32_t len) {
-        uint32_t inc = cnt;
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t t = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += t;
-        }
+    // The group's streams are lanes [l0, l0 + CS) of one 16-lane DPP row
+    // (l0 = 16 k): prefix and min / max by row shifts, without the LDS
+    // bpermutes whose lane-index registers the block scan also keeps live
+    static_assert(CS <= 16 && 16 % CS == 0, "a group's streams lie in one 16-lane row");
+    auto publish = [&](bool mine, uint32_t i, uint32_t c0, uint32_t cnt, int32_t dbias, uint32_t len, uint32_t l0) {
+        uint32_t inc = cnt;  // inclusive prefix within the row (out-of-row lanes read 0)
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x111, 0xF, 0xF, true);  // row_shr:1
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x112, 0xF, 0xF, true);  // row_shr:2
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x114, 0xF, 0xF, true);  // row_shr:4
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x118, 0xF, 0xF, true);  // row_shr:8
         if (mine) {
             cpre[i + 1] = inc;
             clo[i] = c0;
@@ -875,14 +879,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             if (i < CS)
                 ilm[i] = mine && cnt ? make_int4((int32_t)c0, (int32_t)(c0 + cnt), dbias, dbias + (int32_t)len)
                                      : make_int4(0, 0, 0, 0);
-            uint32_t qa = cnt ? c0 : 0xFFFFFFFFu, qb = cnt ? c0 + cnt : 0u;
-            for (uint32_t d = 1; d < 64; d <<= 1) {
-                qa = min(qa, (uint32_t)__shfl_xor(qa, d, 64));
-                qb = max(qb, (uint32_t)__shfl_xor(qb, d, 64));
-            }
-            if (lane == 0) {
-                crng[0] = qa;
-                crng[1] = qb;
+            int32_t qa = cnt ? (int32_t)c0 : 0x7FFFFFFF, qb = cnt ? (int32_t)(c0 + cnt) : 0;
+            // (out-of-row lanes keep the identity passed as the old value)
+            qa = min(qa, __builtin_amdgcn_update_dpp(0x7FFFFFFF, qa, 0x111, 0xF, 0xF, false));
+            qb = max(qb, __builtin_amdgcn_update_dpp(0, qb, 0x111, 0xF, 0xF, false));
+            qa = min(qa, __builtin_amdgcn_update_dpp(0x7FFFFFFF, qa, 0x112, 0xF, 0xF, false));
+            qb = max(qb, __builtin_amdgcn_update_dpp(0, qb, 0x112, 0xF, 0xF, false));
+            qa = min(qa, __builtin_amdgcn_update_dpp(0x7FFFFFFF, qa, 0x114, 0xF, 0xF, false));
+            qb = max(qb, __builtin_amdgcn_update_dpp(0, qb, 0x114, 0xF, 0xF, false));
+            qa = min(qa, __builtin_amdgcn_update_dpp(0x7FFFFFFF, qa, 0x118, 0xF, 0xF, false));
+            qb = max(qb, __builtin_amdgcn_update_dpp(0, qb, 0x118, 0xF, 0xF, false));
+            if (lane == l0 + 15) {  // the row's last lane holds the row's min / max
+                crng[0] = (uint32_t)qa;
+                crng[1] = (uint32_t)qb;
             }
         }
     };
@@ -924,7 +933,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         const uint64_t win0 = (uint64_t)wi * CWIN;
         if (mine && g_r1 > g_r0) chunk_range(off, L, g_ua0, win0, min(g_span, win0 + (uint64_t)CWIN), c0, cnt);
         const int32_t dbias = (int32_t)((int64_t)((uintptr_t)dbase + off - g_ua0) - (int64_t)win0);
-        if (wv == (s0 - blk * 256) / 64) publish(mine, i, c0, cnt, dbias, L);  // the group's wave (uniform branch)
+        if (wv == (s0 - blk * 256) / 64) publish(mine, i, c0, cnt, dbias, L, l0);  // the group's wave (uniform branch)
     }
     __syncthreads();
     const uint64_t r0 = soff[0], r1 = soff[ns - 1] + slen[ns - 1];
@@ -939,16 +948,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         const uint64_t wend = min(span, win + (uint64_t)CWIN);
         const uint32_t wl = (uint32_t)(wend - win);
         if (win != (uint64_t)wi * CWIN) {  // later windows (long streams): new chunk ranges
-            if (tid < 64) {
+            // (t: a copy of tid the compiler cannot see through, so that it does
+            // not hoist this rare block's LDS addresses out of the window loop
+            // and spill them: 64 VGPRs at 8 waves per SIMD)
+            uint32_t t = tid;
+            asm volatile("" : "+v"(t));
+            if (t < 64) {
                 uint32_t c0 = 0, cnt = 0;
                 int32_t dbias = 0;
                 uint32_t len = 0;
-                if (tid < ns) {
-                    chunk_range(soff[tid], slen[tid], ua0, win, wend, c0, cnt);
-                    dbias = (int32_t)((int64_t)((uintptr_t)dbase + soff[tid] - ua0) - (int64_t)win);
-                    len = slen[tid];
+                if (t < ns) {
+                    chunk_range(soff[t], slen[t], ua0, win, wend, c0, cnt);
+                    dbias = (int32_t)((int64_t)((uintptr_t)dbase + soff[t] - ua0) - (int64_t)win);
+                    len = slen[t];
                 }
-                publish(tid < ns, tid, c0, cnt, dbias, len);
+                publish(t < ns, t, c0, cnt, dbias, len, 0);
             }
             __syncthreads();
         }
