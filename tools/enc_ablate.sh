@@ -1,3 +1,4 @@
+#!/bin/bash
 # Encoder ablations on the diagnostic build (ZR_ABLATE: 1 no scratch stores,
 # 2 conflict-free table reads, 3 both), headline workload, same box
 set -o pipefail
