@@ -971,6 +971,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         // crng[0] + f / CS of stream f % CS.
         const uint32_t nchunks = IL ? (crng[1] > crng[0] ? (crng[1] - crng[0]) * CS : 0u) : cpre[ns];
         const uint32_t qrow0 = IL ? crng[0] : 0u;
+        // IL: f0 and 64 k are multiples of CS, so a lane's stream is lane % CS
+        // for the whole window: its range, once, and its scratch column
+        const int4 mi = IL ? ilm[lane % CS] : make_int4(0, 0, 0, 0);
+        const uint8_t *scol = sbase + (lane % CS) * 16;
         uint32_t si = 0;
         for (uint32_t f0 = wv * 64 * CU_LD; f0 < nchunks; f0 += 256 * CU_LD) {
             v4u v[CU_LD];
@@ -982,14 +986,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                 dpos[k] = 0;
                 const uint8_t *src = sbase;
                 if (IL) {
-                    const uint32_t i = f % CS, c = qrow0 + f / CS;
-                    if (f < nchunks) {
-                        const int4 m = ilm[i];
-                        if ((int32_t)c >= m.x && (int32_t)c < m.y) {
-                            src = sbase + (c * 64 + i) * 16;
-                            dpos[k] = m.z + 16 * (int32_t)c;
-                            nv[k] = (uint32_t)min(16, m.w - dpos[k]);
-                        }
+                    const uint32_t c = qrow0 + f / CS;
+                    if (f < nchunks && (int32_t)c >= mi.x && (int32_t)c < mi.y) {
+                        src = scol + c * 1024;
+                        dpos[k] = mi.z + 16 * (int32_t)c;
+                        nv[k] = (uint32_t)min(16, mi.w - dpos[k]);
                     }
                 } else if (f < nchunks) {
                     while (cpre[si + 1] <= f) si++;
