@@ -38,7 +38,9 @@ struct alignas(16) FseDTab {
     uint32_t cmpl[256];
     // encode entry per symbol: {rcp lo, rcp hi, bias | cmpl << 16, freq | shift << 16}
     uint4 enc[256];
-    // decode slot per state: sym | (freq - 1) << 8 | (slot - start) << 20
+    // decode slot per state: sym | (freq & 4095) << 8 | (slot - start) << 20
+    // (freq 4096, a table of one symbol, is stored as 0: the fast decoder takes
+    // the frequency as is and leaves such tables to the generic lane loop)
     uint32_t slot[4096];
     uint8_t hdr[3 + 5 * 256];  // table_log(12) | nsym:u16 | (sym, freq:u32) pairs
 };
@@ -158,7 +160,7 @@ __device__ void fse_build_table(uint32_t f, FseDTab *d, unsigned long long *sh, 
             shift = sh2 - 1;
             bias = start;
         }
-        for (uint32_t i = 0; i < nf; i++) d->slot[start + i] = v | ((nf - 1) << 8) | (i << 20);
+        for (uint32_t i = 0; i < nf; i++) d->slot[start + i] = v | ((nf & 4095) << 8) | (i << 20);
         uint8_t *e = d->hdr + 3 + 5 * rank;
         e[0] = (uint8_t)v;
         e[1] = (uint8_t)norm;
@@ -684,7 +686,8 @@ __device__ __forceinline__ void fse_dec_lane(const uint32_t *slot, const uint8_t
     }
     auto step = [&]() -> uint32_t {
         const uint32_t e = slot[x & 4095];
-        x = (uint64_t)(((e >> 8) & 4095) + 1) * (x >> 12) + (e >> 20);
+        const uint32_t fq = (e >> 8) & 4095;
+        x = (uint64_t)(fq ? fq : 4096u) * (x >> 12) + (e >> 20);
         if (x < 65536 && bp > 0) {
             if (bp >= 4) {
                 bp -= 4;
@@ -754,7 +757,7 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
     FseBlk B = {};
     if (j < nb) B = a.blk[j];
     const bool coded = j < nb && B.raw == 0 && B.orig > 0;
-    const bool fast = coded && B.table == 0;
+    const bool fast = coded && B.table == 0 && T0->nsym > 1;  // (one symbol: freq 4096, generic loop)
     uint8_t *out = a.out + (j < nb ? a.ooff[j] : 0);
 
     const fv4u *in4 = reinterpret_cast<const fv4u *>(a.in - (((uintptr_t)a.in) & 15));
@@ -788,7 +791,7 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
     uint32_t nw = fast && bp >= 4 ? read_word(m) : 0u;
     auto step = [&]() -> uint32_t {
         const uint32_t e = s_slot[x & 4095];
-        x = (uint64_t)(((e >> 8) & 4095) + 1) * (x >> 12) + (e >> 20);
+        x = (uint64_t)((e >> 8) & 4095) * (x >> 12) + (e >> 20);
         // the common 32-bit renormalisation, branchless: the next word is
         // re-read from the ring every step (LDS bandwidth is idle here)
         const bool small = x < 65536;
@@ -817,11 +820,12 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
     auto step_bulk = [&](uint32_t &m32) -> uint32_t {
         const uint32_t w = read_word(m32);
         const uint32_t e = s_slot[x & 4095];
-        const uint32_t w1 = max(w, 1u);
-        const uint64_t xd = (uint64_t)(((e >> 8) & 4095) + 1) * (x >> 12) + (e >> 20);
+        const uint64_t xd = (uint64_t)((e >> 8) & 4095) * (x >> 12) + (e >> 20);
         const bool small = xd < 65536;
         const uint32_t xl = (uint32_t)xd;
-        const uint64_t merged = ((uint64_t)xl << 32) | (xl == 0 ? w1 : w);
+        // max(x, 1) after the merge: the low word is max(w, [xl == 0]), with
+        // [xl == 0] = 1 -sat xl (one clamped subtract)
+        const uint64_t merged = ((uint64_t)xl << 32) | max(w, __builtin_elementwise_sub_sat(1u, xl));
         x = small ? merged : xd;
         m32 -= small ? 1 : 0;
         return e & 0xFF;
