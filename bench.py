@@ -443,7 +443,7 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
                  {"workload": f"{R} x 1 KiB records per GPU, rANS x1 per record, shared trained table",
                   "records": R, "parallelism": f"shard{world}"},
                  _roofline(dom, dom_ms, {"rans_decode_x1": comp + total, "rans_encode_x1": total + comp}, "blob",
-                           {"rans_decode_x1": "k_dec_x1_ring", "rans_encode_x1": "k_enc_x1_fast"}), extra)
+                           {"rans_decode_x1": "k_dec_x1_fast", "rans_encode_x1": "k_enc_x1_fast"}), extra)
 
 
 

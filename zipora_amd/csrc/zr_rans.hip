@@ -1686,18 +1686,33 @@ __device__ bool x1_dec_generic(const RansDTab *T, const uint32_t *stab, bool nor
 // the generic per-lane loop.
 constexpr uint32_t X1W = 512;  // records per workgroup
 constexpr uint32_t X1R = 8;    // ring chunks per lane
-__global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t *raw, KArgs a) {
+// the records k_dec_x1_fast takes
+__device__ __forceinline__ bool x1_fast_ok(uint64_t n, uint64_t len, uint64_t X, const uint8_t *out, bool normal) {
+    // (positions * 8 are kept in 32 bits: records below 2^28 bytes)
+    return n > 0 && len >= 8 && normal && X >= RANS_L && X < (1ull << 24) && len < (1ull << 28) &&
+           n < (1ull << 28) && (((uintptr_t)out) & 15) == 0;
+}
+
+// skip_fast: the records k_dec_x1_fast takes (x1_fast_ok) are left to it
+__global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t *raw, KArgs a, int skip_fast) {
     __shared__ uint32_t stab[TOTFREQ];
     __shared__ uint32_t ring[X1R * 4 * X1W];
     const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);
-    for (uint32_t j = threadIdx.x; j < TOTFREQ; j += X1W) stab[j] = T->slot[j];
     const bool normal = T->kind == DT_NORMAL;
-    __syncthreads();
     const uint32_t tid = threadIdx.x;
     const uint32_t b = blockIdx.x * X1W + tid;
-    if (b >= a.B) return;
+    bool mine = b < a.B && single_mode(a.len[b], a.N);
+    if (mine && skip_fast) {
+        const uint64_t n0 = a.len[b], len0 = a.enc_len[b];
+        const uint8_t *e0 = enc + a.enc_off[b];
+        const uint64_t X0 = (n0 && len0 >= 8) ? ld_u64_u(e0 + len0 - 8) : 0;
+        mine = !x1_fast_ok(n0, len0, X0, raw + a.raw_off[b], normal);
+    }
+    if (!__syncthreads_or(mine)) return;  // (workgroup-uniform) nothing left for this kernel
+    for (uint32_t j = threadIdx.x; j < TOTFREQ; j += X1W) stab[j] = T->slot[j];
+    __syncthreads();
+    if (!mine) return;
     const uint64_t n = a.len[b];
-    if (!single_mode(n, a.N)) return;
     if (n == 0) {  // (x1 buffers: this kernel is the only status writer)
         a.status[b] = ZR_OK;
         return;
@@ -1818,6 +1833,247 @@ __global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t
     a.status[b] = err ? ZR_INVALID_INPUT : ZR_OK;
 }
 
+// ----------------------------------------------------------------------
+// x1 decode, 1024 records per workgroup (decode_single, rans.rs:523-545, for
+// the record batches of RansBlobStore / RansCompressor). One lane = one record,
+// decoded with k_dec_xn_fast's step: renormalisation from a 4-byte window by
+// one 64-bit shift, one ring read per pair of steps, 64-B segment refills that
+// land two tiles after they are issued, a 16 KiB slot table plus a 33-row ring
+// (148 KiB, one workgroup per CU, 16 waves). What differs is the output: a
+// record's bytes are contiguous, so a tile's 16 symbols gather into four dwords
+// (v_perm) and every 8 tiles leave as one whole 128-B line per lane.
+//   * A wave runs tiles up to its longest record. A group of 8 tiles in which
+//     every fast lane of the wave is live ends with eight unconditional 16-B
+//     stores, and the waits below count them. Other groups store per lane
+//     (whole line, dwords, bytes), then wait for all memory operations
+//     (vmcnt(0)), after which the counts hold again.
+//   * The record's lanes this kernel takes: x1_fast_ok. The others (a state
+//     outside [2^16, 2^24), a table that is not DT_NORMAL, an output not
+//     16-B aligned, empty or short records) are k_dec_x1_ring's; a lane whose
+//     reads outran its ring decodes again with x1_dec_generic.
+// ----------------------------------------------------------------------
+constexpr uint32_t XF = 1024;  // records per workgroup
+constexpr uint32_t XG = 8;     // tiles per output group (16 * XG bytes per lane per store run)
+constexpr uint32_t NSET = 1;   // staging register sets: a refill lands NSET boundaries after its loads
+
+__global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t *raw, KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[TOTFREQ + (RR + 1) * XF];
+    const uint32_t tid = threadIdx.x;
+    uint32_t *const lring = lds + TOTFREQ + tid;
+    const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
+    {
+        const v4u *src = reinterpret_cast<const v4u *>(T->slot);
+        v4u *dst = reinterpret_cast<v4u *>(lds);
+        for (uint32_t j = tid; j < TOTFREQ / 4; j += XF) dst[j] = src[j];
+    }
+    const bool normal = T->kind == DT_NORMAL;
+    __syncthreads();
+    // persistent waves: each takes groups of 64 consecutive records in turn, so a
+    // wave that finishes early starts its next group at once (no workgroup tail)
+    const uint32_t ngroups = (a.B + 63) / 64, wstride = gridDim.x * (XF / 64);
+    for (uint32_t q = blockIdx.x * (XF / 64) + (tid >> 6); q < ngroups; q += wstride) {
+    const uint32_t b = q * 64 + (tid & 63);
+    const bool inb = b < a.B;
+    const uint64_t n = inb ? a.len[b] : 0;
+    const bool mine = inb && single_mode(n, a.N);
+    const uint64_t len = mine ? a.enc_len[b] : 0;
+    const uint8_t *e = enc + (mine ? a.enc_off[b] : 0);
+    uint8_t *const out = raw + (mine ? a.raw_off[b] : 0);
+    const uint64_t X = (mine && n && len >= 8) ? ld_u64_u(e + len - 8) : 0;
+    const bool fast = mine && x1_fast_ok(n, len, X, out, normal);
+    const uint32_t nn = fast ? (uint32_t)n : 0u;
+    // the wave's shortest and longest fast record
+    uint32_t cmin = fast ? nn : 0xFFFFFFFFu, cmax = nn;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        cmin = min(cmin, (uint32_t)__shfl_xor(cmin, d, 64));
+        cmax = max(cmax, (uint32_t)__shfl_xor(cmax, d, 64));
+    }
+    if (cmax == 0) continue;  // (wave-uniform) no record of this group is ours
+    const uintptr_t pend = (uintptr_t)e + (len - 8);
+    const uintptr_t lo_lim = ((uintptr_t)e) & ~(uintptr_t)63;
+    auto clampa = [&](uintptr_t p) -> uintptr_t { return p > lo_lim ? p : lo_lim; };
+    // lanes that fetch nothing load a line of the table (L2-resident)
+    const uintptr_t dummy = (uintptr_t)T->slot + 64 * (tid >> 6);
+    // write the 64-B segment at absolute address g (64-aligned) into the ring
+    auto put_seg = [&](uint32_t g, const v4u c0, const v4u c1, const v4u c2, const v4u c3) {
+        const uint32_t r0 = ((g >> 2) + 1) & (RR - 1);  // 1 or 17
+        uint32_t *p = lring + r0 * XF;
+        p[0 * XF] = c0.x; p[1 * XF] = c0.y; p[2 * XF] = c0.z; p[3 * XF] = c0.w;
+        p[4 * XF] = c1.x; p[5 * XF] = c1.y; p[6 * XF] = c1.z; p[7 * XF] = c1.w;
+        p[8 * XF] = c2.x; p[9 * XF] = c2.y; p[10 * XF] = c2.z; p[11 * XF] = c2.w;
+        p[12 * XF] = c3.x; p[13 * XF] = c3.y; p[14 * XF] = c3.z;
+        p[15 * XF] = c3.w;                           // row 16, or the mirror row 32
+        lring[((r0 + 15) & (RR - 1)) * XF] = c3.w;  // row 0 itself (r0 = 17; r0 = 1: row 16 again)
+    };
+    // prologue: the 64-B segment holding the record's last stream byte and the one below
+    const uintptr_t g1 = (pend - 1) & ~(uintptr_t)63;
+    {
+        const v4u *p1 = reinterpret_cast<const v4u *>(fast ? clampa(g1) : dummy);
+        const v4u *p0 = reinterpret_cast<const v4u *>(fast ? clampa(g1 - 64) : dummy);
+        const v4u a0 = p1[0], a1 = p1[1], a2 = p1[2], a3 = p1[3];
+        const v4u b0 = p0[0], b1 = p0[1], b2 = p0[2], b3 = p0[3];
+        put_seg((uint32_t)g1, a0, a1, a2, a3);
+        put_seg((uint32_t)(g1 - 64), b0, b1, b2, b3);
+    }
+    uintptr_t lo64 = g1 - 64;              // lowest resident byte
+    uint32_t pos8 = (uint32_t)pend << 3;   // bytes [.., pos) not yet consumed, * 8 (mod 2^32)
+    uint32_t pos_snap = pos8;              // pos8 after the lane's last live step
+    uint32_t x = fast ? (uint32_t)X : RANS_L;
+    bool bad = false;
+    auto readD = [&](uint32_t p8) -> uint32_t {  // the 4 stream bytes below p (byte p-1 on top)
+        const uint32_t *q = lring + ((p8 >> 5) & (RR - 1)) * XF;
+        return __builtin_amdgcn_alignbit(q[XF], q[0], p8);
+    };
+    // one decode step (rans.rs:472-507), as in k_dec_xn_fast
+    auto step = [&](uint32_t D, uint32_t &hi, uint32_t &lo, uint32_t &sft) -> uint32_t {
+        sft = __builtin_clz(x) & 24;
+        const uint64_t t = ((((uint64_t)x) << 32) | D) << sft;
+        hi = (uint32_t)(t >> 32);
+        lo = (uint32_t)t;
+        const uint32_t ent =
+            *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + ((hi >> 6) & 0x3FFC));
+        x = __umul24(ent >> 20, hi >> 20) + ((ent >> 8) & 0xFFF);
+        return ent;
+    };
+    v4u e0 = {0, 0, 0, 0}, e1 = e0, e2 = e0, e3 = e0, f0 = e0, f1 = e0, f2 = e0, f3 = e0;
+    bool pnd = false;  // a segment in flight, fetched at boundary ptile
+    uint32_t ptile = 0;
+    // tile boundary t with staging set s0..s3; WC = memory operations issued after
+    // the loads of boundary t - 2 (4 loads of boundary t - 1, plus a group's
+    // eight stores when one ended in between)
+    auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3, auto wc) {
+        // every read of tile t - 1 (lanes live in it) was at or above pos - 4
+        bad |= fast && 16 * t < nn + 16 && (int32_t)(pos8 - 32 - ((uint32_t)lo64 << 3)) < 0;
+        if (t >= NSET) {
+            asm volatile("s_waitcnt vmcnt(%4)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3) : "i"(decltype(wc)::value) : "memory");
+            if (pnd && ptile + NSET == t) {  // the segment this set fetched at boundary t - NSET
+                lo64 -= 64;
+                put_seg((uint32_t)lo64, s0, s1, s2, s3);
+                pnd = false;
+            }
+        }
+        // a live lane with <= 64 unread resident bytes fetches the segment below
+        const bool issue = fast && 16 * t < nn && !pnd && (int32_t)(pos8 - ((uint32_t)lo64 << 3)) <= 64 * 8;
+        const uintptr_t g = issue ? clampa(lo64 - 64) : dummy;
+        asm_load16(s0, g);
+        asm_load16_off<16>(s1, g);
+        asm_load16_off<32>(s2, g);
+        asm_load16_off<48>(s3, g);
+        if (issue) {
+            pnd = true;
+            ptile = t;
+        }
+    };
+    // DT2 steps in pairs, one ring read per pair; the 16 symbols -> o[0..3].
+    // IRR: some lane may end inside the tile (pos_snap follows its live steps)
+    auto tile = [&](uint32_t t, uint32_t *o, auto irr) {
+        uint32_t D = readD(pos8);
+        uint32_t lo2 = 0;
+#pragma unroll
+        for (int j = 0; j < DT2 / 2; j++) {
+            uint32_t hA, lA, sA, hB, lB, sB;
+            const uint32_t eA = step(D, hA, lA, sA);
+            const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
+            uint32_t used;  // sA + sB - 16 = 8 * bytes consumed by the pair
+            asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
+            if constexpr (decltype(irr)::value) {
+                const uint32_t kA = 16 * t + 2 * j;
+                pos_snap = kA < nn ? pos8 + 8 - sA : pos_snap;
+                pos_snap = kA + 1 < nn ? pos8 - used : pos_snap;
+            }
+            pos8 -= used;
+            if (j + 1 < DT2 / 2) D = readD(pos8);
+            // sym A | sym B << 8, packed as soon as the pair is done (an empty asm
+            // pins it: left to the scheduler, all 16 entries stay live to the
+            // tile's end)
+            uint32_t pr = __builtin_amdgcn_perm(eB, eA, 0x0c0c0400u);
+            asm volatile("" : "+v"(pr));
+            if (j & 1)
+                o[j >> 1] = __builtin_amdgcn_perm(pr, lo2, 0x05040100u);
+            else
+                lo2 = pr;
+        }
+        if constexpr (!decltype(irr)::value) pos_snap = pos8;
+    };
+    // memory operations younger than the loads being waited for: NSET = 2, the 4
+    // loads of boundary t - 1 (+ the previous group's XG stores at the first two
+    // boundaries of a group); NSET = 1, none (+ the XG stores at the first)
+    using W4 = std::integral_constant<int, NSET == 2 ? 4 : 0>;
+    using WG = std::integral_constant<int, NSET == 2 ? 4 + XG : XG>;
+    using WG1 = std::integral_constant<int, NSET == 2 ? 4 + XG : 0>;
+    const uint32_t ntile = (cmax + DT2 - 1) / DT2;
+    const uint32_t ngrp = (ntile + XG - 1) / XG;
+    auto group = [&](uint32_t g, auto irr) {
+        constexpr bool IRR = decltype(irr)::value;
+        uint32_t o[4 * XG];
+        const uint32_t t0 = XG * g;
+        // tile t0 + k exists for k < ntile - t0 (the last group may be short)
+        boundary(t0, e0, e1, e2, e3, WG());
+        tile(t0, o, irr);
+        boundary(t0 + 1, NSET == 2 ? f0 : e0, NSET == 2 ? f1 : e1, NSET == 2 ? f2 : e2, NSET == 2 ? f3 : e3, WG1());
+        tile(t0 + 1, o + 4, irr);
+#pragma unroll
+        for (uint32_t k = 2; k < XG; k += 2) {
+            if (!IRR || t0 + k < ntile) {
+                boundary(t0 + k, e0, e1, e2, e3, W4());
+                tile(t0 + k, o + 4 * k, irr);
+            }
+            if (!IRR || t0 + k + 1 < ntile) {
+                boundary(t0 + k + 1, NSET == 2 ? f0 : e0, NSET == 2 ? f1 : e1, NSET == 2 ? f2 : e2, NSET == 2 ? f3 : e3, W4());
+                tile(t0 + k + 1, o + 4 * k + 4, irr);
+            }
+        }
+        x4u *d = reinterpret_cast<x4u *>(out + 16 * XG * (size_t)g);
+        if constexpr (!IRR) {
+            if (fast) {
+#pragma unroll
+                for (uint32_t k = 0; k < XG; k++) d[k] = x4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+            }
+        } else {
+            if (fast && nn > 16 * XG * g) {
+                const uint32_t full = min(nn - 16 * XG * g, 16 * XG);
+                if (full == 16 * XG) {
+#pragma unroll
+                    for (uint32_t k = 0; k < XG; k++) d[k] = x4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                } else {
+                    uint8_t *db = reinterpret_cast<uint8_t *>(d);
+                    uint32_t wl = 0;  // the dword holding the last bytes
+#pragma unroll
+                    for (uint32_t k = 0; k < 4 * XG; k++) {
+                        if (4 * k + 4 <= full) *reinterpret_cast<uint32_t *>(db + 4 * k) = o[k];
+                        wl = k == (full >> 2) ? o[k] : wl;
+                    }
+                    for (uint32_t i = full & ~3u; i < full; i++) db[i] = (uint8_t)(wl >> (8 * (i & 3)));
+                }
+            }
+            // per-lane stores: resynchronise the vmcnt accounting
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1),
+                         "+v"(f2), "+v"(f3)::"memory");
+        }
+    };
+    const uint32_t nreg = cmin / (16 * XG);  // groups in which every fast lane of the wave is live
+    uint32_t g = 0;
+    for (; g < nreg; g++) group(g, std::false_type());
+    for (; g < ngrp; g++) group(g, std::true_type());
+    // the reads of the wave's last tile (lanes live in it)
+    bad |= fast && 16 * (ntile - 1) < nn && (int32_t)(pos8 - 32 - ((uint32_t)lo64 << 3)) < 0;
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1), "+v"(f2),
+                 "+v"(f3)::"memory");
+    if (fast) {
+        int32_t st;
+        if (bad) {
+            st = x1_dec_generic(T, lds, normal, e, len, X, out, n) ? ZR_OK : ZR_INVALID_INPUT;
+        } else {
+            // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
+            const uint32_t consumed = (((uint32_t)pend << 3) - pos_snap) >> 3;
+            st = consumed > (uint32_t)(len - 8) ? ZR_INVALID_INPUT : ZR_OK;
+        }
+        a.status[b] = st;
+    }
+    }  // groups of 64 records
+}
+
 
 // ======================================================================
 // exhaustive check of the encoder's reciprocal division (the analogue of the
@@ -1914,6 +2170,19 @@ int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t by
 // over as many CUs as there are waves (up to 1024 workgroups: 4 per CU, each
 // with its own 16 KiB table copy, fit the LDS) instead of a few 1024-lane or
 // 256-lane workgroups on a handful of CUs.
+// compute units of the current device (cached per device)
+static uint32_t cu_count() {
+    static int cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return (uint32_t)cached[dev];
+}
+
 static bool narrow_batch(const KArgs &a) { return (uint64_t)a.B * a.N <= (1u << 16); }
 
 static KArgs kargs(const zr_rans_batch *bt) {
@@ -2130,9 +2399,13 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
     }
     timer_begin("rans_decode_x1", s);
     if (!(bt->min_len >= a.N && a.N > 1)) {
-        if (a.table_stride == 0)
-            hipLaunchKernelGGL(k_dec_x1_ring, dim3((uint32_t)ceil_div(a.B, X1W)), dim3(X1W), 0, s, enc, raw, a);
-        else
+        if (a.table_stride == 0) {
+            // k_dec_x1_fast takes the records x1_fast_ok admits, k_dec_x1_ring the rest
+            // one workgroup per CU (148 KiB of LDS each), persistent waves
+            const uint64_t gf = std::min<uint64_t>(ceil_div(a.B, XF), (uint64_t)cu_count());
+            hipLaunchKernelGGL(k_dec_x1_fast, dim3((uint32_t)gf), dim3(XF), 0, s, enc, raw, a);
+            hipLaunchKernelGGL(k_dec_x1_ring, dim3((uint32_t)ceil_div(a.B, X1W)), dim3(X1W), 0, s, enc, raw, a, 1);
+        } else
             hipLaunchKernelGGL(k_dec_x1_generic, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, enc, raw, a);
     }
     timer_end("rans_decode_x1", s);
