@@ -29,6 +29,11 @@ timeout -k 10 300 rocprofv3 $K --pmc WRITE_SIZE --output-format csv -d $O/pmc_li
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/fse -o fse -- python3 bench.py --workload fse --steps 5 --warmup 2 --no-cpu-baseline > $O/fse_bench.log 2>&1
 timeout -k 10 300 rocprofv3 $K --pmc FETCH_SIZE --output-format csv -d $O/pmc_fse_fetch -o fetch -- python3 bench.py --workload fse --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_fse_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 $K --pmc WRITE_SIZE --output-format csv -d $O/pmc_fse_write -o write -- python3 bench.py --workload fse --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_fse_write.log 2>&1
+# 3b. record batch (configs[4]) and O1 shard (configs[3]) traffic
+timeout -k 10 300 rocprofv3 $K --pmc FETCH_SIZE --output-format csv -d $O/pmc_blob_fetch -o fetch -- python3 bench.py --workload blob --steps 1 --warmup 1 --no-cpu-baseline --no-host-path > $O/pmc_blob_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 $K --pmc WRITE_SIZE --output-format csv -d $O/pmc_blob_write -o write -- python3 bench.py --workload blob --steps 1 --warmup 1 --no-cpu-baseline --no-host-path > $O/pmc_blob_write.log 2>&1
+timeout -k 10 300 rocprofv3 $K --pmc FETCH_SIZE --output-format csv -d $O/pmc_o1_fetch -o fetch -- python3 bench.py --workload o1 --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_o1_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 $K --pmc WRITE_SIZE --output-format csv -d $O/pmc_o1_write -o write -- python3 bench.py --workload o1 --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_o1_write.log 2>&1
 # 4. O1 shard (configs[3]) and record batch (configs[4]) kernel traces
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/o1 -o o1 -- python3 bench.py --workload o1 --steps 10 --warmup 3 --no-cpu-baseline > $O/o1_bench.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/blob -o blob -- python3 bench.py --workload blob --steps 3 --warmup 1 --no-cpu-baseline --no-host-path > $O/blob_bench.log 2>&1

@@ -1519,7 +1519,7 @@ __global__ __launch_bounds__(64) void k_dec_x1_generic(const uint8_t *enc, uint8
 // ----------------------------------------------------------------------
 typedef unsigned x4u __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t *enc, KArgs a, RansWork w) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_enc_x1_fast(const uint8_t *raw, uint8_t *enc, KArgs a, RansWork w) {
     __shared__ uint4 et[256];
     const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
     {
@@ -1600,23 +1600,67 @@ __global__ __launch_bounds__(256) void k_enc_x1_fast(const uint8_t *raw, uint8_t
     if (full) {
         int64_t c = (int64_t)(full >> 4) - 1;
         if ((((uintptr_t)in) & 15) == 0) {
-            const x4u *in4 = reinterpret_cast<const x4u *>(in);
+            // The record is read in whole 64-B blocks of the absolute address
+            // (4 chunks of 16 symbols), the block below loaded while this one is
+            // coded. A lane's 16-B loads one chunk apart had refetched each
+            // input line up to 8 times: 1024 lanes per CU read 1024 different
+            // lines, as many as the XCD's L2 holds, and the line was gone before
+            // its next chunk was needed (FETCH 6.1 GB per GiB of records).
+            // Blocks only hold bytes of the record or of its 64-B neighbourhood
+            // (same page), and a block below the record's start is never loaded.
+            // (pointer arithmetic from `in`, not integer casts: the loads stay
+            // global_load, not flat loads whose waits also cover the LDS reads)
+            const uint8_t *blk = in + 16 * c - (((uintptr_t)(in + 16 * c)) & 63);  // the top chunk's block
+            const x4u *cb = reinterpret_cast<const x4u *>(blk);
+            x4u w0 = cb[0], w1 = cb[1], w2 = cb[2], w3 = cb[3];
             const x4u z = {0, 0, 0, 0};
-            x4u cur = in4[c];
-            x4u n1 = c >= 1 ? in4[c - 1] : z;
-            for (; c >= 0; c--) {
-                const x4u wv = cur;
-                cur = n1;
-                if (c >= 2) n1 = in4[c - 2];
-                uint4 e[16];
+            const bool more = blk > in;  // the block below holds record bytes
+            x4u m0 = more ? cb[-4] : z, m1 = more ? cb[-3] : z, m2 = more ? cb[-2] : z, m3 = more ? cb[-1] : z;
+            auto enc16 = [&](const x4u wv) __attribute__((always_inline)) {
 #pragma unroll
-                for (int k = 15; k >= 0; k--) e[k] = et[(wv[k >> 2] >> (8 * (k & 3))) & 0xFF];
-#pragma unroll
-                for (int k = 15; k >= 0; k--) {
-                    enc_step(e[k]);
-                    if (k & 1) push();
+                for (int g = 3; g >= 0; g--) {  // table entries four at a time (16 VGPRs, not 64)
+                    const uint32_t w = wv[g];
+                    const uint4 e3 = et[w >> 24], e2 = et[(w >> 16) & 0xFF], e1 = et[(w >> 8) & 0xFF],
+                                e0 = et[w & 0xFF];
+                    enc_step(e3);
+                    enc_step(e2);
+                    push();
+                    enc_step(e1);
+                    enc_step(e0);
+                    push();
                 }
                 push();
+            };
+            // the top block from chunk c's place p down (chunk c - p + k at place k;
+            // places below the record's first chunk are not the record's)
+            {
+                const uint32_t p = (uint32_t)((((uintptr_t)in) >> 4) + (uint64_t)c) & 3;
+                const int64_t c0 = c - (int64_t)p;
+                if (p >= 3) enc16(w3);
+                if (p >= 2 && c0 + 2 >= 0) enc16(w2);
+                if (p >= 1 && c0 + 1 >= 0) enc16(w1);
+                if (c0 >= 0) enc16(w0);
+                c = c0 - 1;
+            }
+            // whole blocks below (chunk c at the block's top); the lowest may start
+            // inside the record's first block
+            while (c >= 0) {
+                w0 = m0;
+                w1 = m1;
+                w2 = m2;
+                w3 = m3;
+                cb -= 4;
+                if (reinterpret_cast<const uint8_t *>(cb) > in) {
+                    m0 = cb[-4];
+                    m1 = cb[-3];
+                    m2 = cb[-2];
+                    m3 = cb[-1];
+                }
+                enc16(w3);
+                if (c >= 1) enc16(w2);
+                if (c >= 2) enc16(w1);
+                if (c >= 3) enc16(w0);
+                c -= 4;
             }
         } else {
             for (uint64_t i = full; i-- > 0;) {
@@ -1693,21 +1737,15 @@ __device__ __forceinline__ bool x1_fast_ok(uint64_t n, uint64_t len, uint64_t X,
            n < (1ull << 28) && (((uintptr_t)out) & 15) == 0;
 }
 
-// skip_fast: the records k_dec_x1_fast takes (x1_fast_ok) are left to it
-__global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t *raw, KArgs a, int skip_fast) {
+// taken (non-null): the records k_dec_x1_fast decoded (taken[b] != 0) are left to it
+__global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t *raw, KArgs a, const uint32_t *taken) {
     __shared__ uint32_t stab[TOTFREQ];
     __shared__ uint32_t ring[X1R * 4 * X1W];
     const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);
     const bool normal = T->kind == DT_NORMAL;
     const uint32_t tid = threadIdx.x;
     const uint32_t b = blockIdx.x * X1W + tid;
-    bool mine = b < a.B && single_mode(a.len[b], a.N);
-    if (mine && skip_fast) {
-        const uint64_t n0 = a.len[b], len0 = a.enc_len[b];
-        const uint8_t *e0 = enc + a.enc_off[b];
-        const uint64_t X0 = (n0 && len0 >= 8) ? ld_u64_u(e0 + len0 - 8) : 0;
-        mine = !x1_fast_ok(n0, len0, X0, raw + a.raw_off[b], normal);
-    }
+    const bool mine = b < a.B && single_mode(a.len[b], a.N) && !(taken && taken[b]);
     if (!__syncthreads_or(mine)) return;  // (workgroup-uniform) nothing left for this kernel
     for (uint32_t j = threadIdx.x; j < TOTFREQ; j += X1W) stab[j] = T->slot[j];
     __syncthreads();
@@ -1856,7 +1894,11 @@ constexpr uint32_t XF = 1024;  // records per workgroup
 constexpr uint32_t XG = 8;     // tiles per output group (16 * XG bytes per lane per store run)
 constexpr uint32_t NSET = 1;   // staging register sets: a refill lands NSET boundaries after its loads
 
-__global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t *raw, KArgs a) {
+// taken[b] (workspace, one word per buffer): 1 for the records this kernel
+// decodes, 0 for the other x1 records (k_dec_x1_ring's), so that kernel need not
+// re-derive x1_fast_ok (the records' offsets and final states: 134 MB of reads
+// for a million records)
+__global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t *raw, KArgs a, uint32_t *taken) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[TOTFREQ + (RR + 1) * XF];
     const uint32_t tid = threadIdx.x;
     uint32_t *const lring = lds + TOTFREQ + tid;
@@ -1881,6 +1923,7 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
     uint8_t *const out = raw + (mine ? a.raw_off[b] : 0);
     const uint64_t X = (mine && n && len >= 8) ? ld_u64_u(e + len - 8) : 0;
     const bool fast = mine && x1_fast_ok(n, len, X, out, normal);
+    if (mine) taken[b] = fast ? 1u : 0u;
     const uint32_t nn = fast ? (uint32_t)n : 0u;
     // the wave's shortest and longest fast record
     uint32_t cmin = fast ? nn : 0xFFFFFFFFu, cmax = nn;
@@ -2403,8 +2446,9 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
             // k_dec_x1_fast takes the records x1_fast_ok admits, k_dec_x1_ring the rest
             // one workgroup per CU (148 KiB of LDS each), persistent waves
             const uint64_t gf = std::min<uint64_t>(ceil_div(a.B, XF), (uint64_t)cu_count());
-            hipLaunchKernelGGL(k_dec_x1_fast, dim3((uint32_t)gf), dim3(XF), 0, s, enc, raw, a);
-            hipLaunchKernelGGL(k_dec_x1_ring, dim3((uint32_t)ceil_div(a.B, X1W)), dim3(X1W), 0, s, enc, raw, a, 1);
+            hipLaunchKernelGGL(k_dec_x1_fast, dim3((uint32_t)gf), dim3(XF), 0, s, enc, raw, a, w.st_state);
+            hipLaunchKernelGGL(k_dec_x1_ring, dim3((uint32_t)ceil_div(a.B, X1W)), dim3(X1W), 0, s, enc, raw, a,
+                               (const uint32_t *)w.st_state);
         } else
             hipLaunchKernelGGL(k_dec_x1_generic, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, enc, raw, a);
     }
