@@ -12,6 +12,7 @@
 // is staged through an LDS tile and moved with 16-byte coalesced accesses.
 // The decode slot table (16 KiB) and encode symbol table (2 KiB) live in LDS.
 // Per-buffer x1 streams (blob records) run one lane per buffer.
+#include <atomic>
 #include <cstdlib>
 
 #include "zr_internal.h"
@@ -1165,35 +1166,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
 // ABL: diagnostic ablations for profiling only, ZR_DIAG builds (1: no output
 // stores, 2: no slot table read, 4: no ring refills, 8: per-workgroup timeline
 // records written to the workspace scratch area); the product instantiates ABL = 0.
+//
+// epoch (non-zero): this kernel also does k_dec_hdr's work (nblk <= SCAN_FUSE):
+// every workgroup reads all N stream lengths of its buffer for its own offset
+// and the buffer's checks, workgroup 0 of the buffer writes the call's first
+// status and then publishes `epoch` (unique per call) in the buffer's flag word
+// (blockoff[b * nblk], unused at this nblk); a workgroup that finds an error
+// waits for that flag before it stores ZR_INVALID_INPUT, so no OK overwrites
+// an error (the wait never spins in practice: workgroup 0 writes at its start,
+// errors come at the end). epoch == 0: k_dec_hdr (and k_scan) ran first.
 template <int FW, int ABL, bool WT = false>
 __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
-                                               uint32_t nblkF) {
+                                               uint32_t nblkF, uint64_t epoch) {
     const uint32_t b = blockIdx.x / nblkF, blkF = blockIdx.x % nblkF;
     const uint64_t dbg_t0 = (ABL & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t dbg_c0 = (ABL & 8) ? __builtin_amdgcn_s_memtime() : 0;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
     const uint32_t N = a.N;
-    if (n == 0 || single_mode(n, N) || a.status[b] != 0) return;
-    // the buffer's scan of block length sums (k_scan, fused for nblk <= SCAN_FUSE
-    // blocks: every wave sums the <= 64 block sums itself) and its check
-    // "Invalid stream data length" (rans.rs:608-610), before any stream read
+    if (n == 0 || single_mode(n, N)) return;
+    if (!epoch && a.status[b] != 0) return;  // k_dec_hdr found the header invalid
     const uint32_t nblk = w.nblk;
-    uint64_t blo;
-    {
-        const uint32_t blk0 = (blockIdx.x % nblkF) * FW / 256;
-        if (nblk <= SCAN_FUSE) {
-            const uint32_t l = threadIdx.x & 63;
-            const uint64_t v = l < nblk ? w.blocksum[(size_t)b * nblk + l] : 0;
-            blo = wave_sum(l < blk0 ? v : 0);
-            if ((uint64_t)N * 12 + wave_sum(v) > a.enc_len[b]) {  // workgroup-uniform
-                if (threadIdx.x == 0) a.status[b] = ZR_INVALID_INPUT;
-                return;
-            }
-        } else {
-            blo = w.blockoff[(size_t)b * nblk + blk0];
-        }
-    }
+    uint64_t *const eflag = w.blockoff + (size_t)b * nblk;  // (epoch mode)
     // slot table: 4-byte entries (sym | (slot - start) << 8 | f << 20). WT (the
     // one-wave shape when at most 3 workgroups share a CU: LDS to spare) keeps
     // 8-byte entries instead, {f | sym << 24, slot - start}, so the update is one
@@ -1221,11 +1215,77 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             for (uint32_t j = tid; j < TOTFREQ / 4; j += FW) dst[j] = src[j];
         }
     }
+    const uint8_t *e = enc + a.enc_off[b];
+    const bool len4 = ((((uintptr_t)e) | N) & 3) == 0;  // the length array is dword-aligned
+    auto stream_len = [&](uint32_t i) -> uint32_t {
+        const uint8_t *p = e + 8 * (size_t)N + 4 * (size_t)i;
+        return len4 ? *reinterpret_cast<const uint32_t *>(p) : ld_u32_u(p);
+    };
+    // blo: the bytes of the buffer's streams below this workgroup's first one
+    uint64_t blo;
+    if (epoch) {
+        // min_header_size (rans.rs:563-568), then "Invalid stream data length"
+        // (rans.rs:608-610), before any stream read
+        const bool hdr_ok = a.enc_len[b] >= (uint64_t)N * 12;
+        const uint32_t first = blkF * FW;
+        uint64_t lo = 0, tot = 0;
+        if (hdr_ok) {
+            for (uint32_t i = tid; i < N; i += FW) {
+                const uint32_t v = stream_len(i);
+                tot += v;
+                lo += i < first ? v : 0u;
+            }
+        }
+        lo = wave_sum(lo);
+        tot = wave_sum(tot);
+        if (FW > 64) {
+            if ((tid & 63) == 0) {
+                sh[2 * (tid >> 6)] = lo;
+                sh[2 * (tid >> 6) + 1] = tot;
+            }
+            __syncthreads();
+            lo = tot = 0;
+            for (uint32_t i = 0; i < FW / 64; i++) {
+                lo += sh[2 * i];
+                tot += sh[2 * i + 1];
+            }
+            __syncthreads();
+        }
+        const bool ok = hdr_ok && (uint64_t)N * 12 + tot <= a.enc_len[b];
+        if (blkF == 0 && tid == 0) {  // the call's first status write for this buffer
+            a.status[b] = ok ? ZR_OK : ZR_INVALID_INPUT;
+            __hip_atomic_store(eflag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!ok) return;  // (workgroup-uniform)
+        blo = lo;
+    } else {
+        // the scan of k_dec_hdr's block sums (fused for nblk <= SCAN_FUSE: every
+        // wave sums the <= 64 block sums itself) and the total check
+        const uint32_t blk0 = (blockIdx.x % nblkF) * FW / 256;
+        if (nblk <= SCAN_FUSE) {
+            const uint32_t l = threadIdx.x & 63;
+            const uint64_t v = l < nblk ? w.blocksum[(size_t)b * nblk + l] : 0;
+            blo = wave_sum(l < blk0 ? v : 0);
+            if ((uint64_t)N * 12 + wave_sum(v) > a.enc_len[b]) {  // workgroup-uniform
+                if (threadIdx.x == 0) a.status[b] = ZR_INVALID_INPUT;
+                return;
+            }
+        } else {
+            blo = w.blockoff[(size_t)b * nblk + blk0];
+        }
+    }
+    // an error of this workgroup: ZR_INVALID_INPUT once the call's first status
+    // write is visible (epoch mode)
+    auto set_invalid = [&]() {
+        if (epoch)
+            while (__hip_atomic_load(eflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+                __builtin_amdgcn_s_sleep(8);
+        a.status[b] = ZR_INVALID_INPUT;
+    };
     const uint32_t kind = T->kind;
     const uint32_t s = blkF * FW + tid;
     const bool active = s < N;
-    const uint8_t *e = enc + a.enc_off[b];
-    const uint32_t L = active ? ld_u32_u(e + 8 * (size_t)N + 4 * (size_t)s) : 0;
+    const uint32_t L = active ? stream_len(s) : 0;
     const unsigned long long inc = wave_incl_scan(L);
     const int wv = tid >> 6;
     if ((tid & 63) == 63) sh[wv] = inc;
@@ -1237,7 +1297,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // lengths of the block's streams below this workgroup
     const uint32_t blk0 = (blkF * FW) / 256, below = (blkF * FW) % 256;
     uint64_t sub = 0;
-    if (FW < 256 && below) {
+    if (FW < 256 && below && !epoch) {  // (epoch mode: blo covers them)
         uint64_t v = 0;
         for (uint32_t i = tid; i < below; i += FW) v += ld_u32_u(e + 8 * (size_t)N + 4 * ((size_t)blk0 * 256 + i));
         sub = wave_sum(v);  // FW < 256 is one wave
@@ -1258,7 +1318,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // below, a lane whose reads outran its ring
     auto generic = [&]() {
         if (!dec_lane_generic(T, T->slot, reinterpret_cast<const uint8_t *>(sb), L, X, c, obuf, N, s))
-            a.status[b] = ZR_INVALID_INPUT;
+            set_invalid();
     };
     if (any_slow) {
         if (active) generic();
@@ -1470,7 +1530,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             } else {
                 // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
                 const uint32_t consumed = (((uint32_t)pend << 3) - pos_snap) >> 3;
-                if (consumed > L) a.status[b] = ZR_INVALID_INPUT;
+                if (consumed > L) set_invalid();
             }
         }
     }
@@ -2213,6 +2273,15 @@ int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t by
 // over as many CUs as there are waves (up to 1024 workgroups: 4 per CU, each
 // with its own 16 KiB table copy, fit the LDS) instead of a few 1024-lane or
 // 256-lane workgroups on a handful of CUs.
+// a per-call tag, never 0, never repeated in the process (k_dec_xn_fast's
+// first-status flag: a flag word left by an earlier call holds an older value)
+static uint64_t next_epoch() {
+    static std::atomic<uint64_t> ctr{0x9E3779B97F4A7C15ull};
+    uint64_t v;
+    do v = ctr.fetch_add(1, std::memory_order_relaxed) + 1; while (v == 0);
+    return v;
+}
+
 // compute units of the current device (cached per device)
 static uint32_t cu_count() {
     static int cached[64] = {};
@@ -2405,22 +2474,27 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
     int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
     if (st) return st;
     hipStream_t s = (hipStream_t)stream;
-    // (no status memset: k_dec_hdr writes the status of xN buffers first, later
-    // kernels only ever set ZR_INVALID_INPUT; the x1 decoder writes the others)
+    // (no status memset: the first status write of an xN buffer is the decoder's
+    // workgroup 0 (or k_dec_hdr above SCAN_FUSE blocks), later writes only ever
+    // set ZR_INVALID_INPUT; the x1 decoders write the others)
     const uint64_t gx = (uint64_t)w.nblk * a.B;
+    uint64_t epoch = 0;
     if (bt->max_len >= a.N && a.N > 1) {
-        hipLaunchKernelGGL(k_dec_hdr, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
-        if (w.nblk > SCAN_FUSE)  // (otherwise the decoder scans the block sums itself)
+        if (w.nblk > SCAN_FUSE) {  // the block sums and their scan first
+            hipLaunchKernelGGL(k_dec_hdr, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
             hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
+        } else {  // the decoder reads the lengths itself (see k_dec_xn_fast)
+            epoch = next_epoch();
+        }
         if (narrow_batch(a)) {
             const uint32_t nblkF = (uint32_t)ceil_div(a.N, 64);
             // (8-byte slot entries while the workgroups fit three per CU)
             if ((uint64_t)nblkF * a.B <= 3 * 256)
                 launch_timed("rans_decode", k_dec_xn_fast<64, 0, true>, dim3(nblkF * a.B), dim3(64), 0, s, enc, raw, a,
-                             w, nblkF);
+                             w, nblkF, epoch);
             else
                 launch_timed("rans_decode", k_dec_xn_fast<64, 0, false>, dim3(nblkF * a.B), dim3(64), 0, s, enc, raw,
-                             a, w, nblkF);
+                             a, w, nblkF, epoch);
         } else {
             const uint32_t nblkF = (uint32_t)ceil_div(a.N, 1024);
 #ifdef ZR_DIAG
@@ -2437,7 +2511,7 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
 #else
             auto kern = k_dec_xn_fast<1024, 0>;
 #endif
-            launch_timed("rans_decode", kern, dim3(nblkF * a.B), dim3(1024), 0, s, enc, raw, a, w, nblkF);
+            launch_timed("rans_decode", kern, dim3(nblkF * a.B), dim3(1024), 0, s, enc, raw, a, w, nblkF, epoch);
         }
     }
     timer_begin("rans_decode_x1", s);
