@@ -1579,7 +1579,9 @@ __global__ __launch_bounds__(64) void k_dec_x1_generic(const uint8_t *enc, uint8
 // ----------------------------------------------------------------------
 typedef unsigned x4u __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_enc_x1_fast(const uint8_t *raw, uint8_t *enc, KArgs a, RansWork w) {
+// skip_ring: the records k_enc_x1_ring takes (x1_enc_ok) are left to it
+__device__ __forceinline__ bool x1_enc_ok(const uint8_t *in, const uint8_t *out, uint64_t n);
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_enc_x1_fast(const uint8_t *raw, uint8_t *enc, KArgs a, int skip_ring) {
     __shared__ uint4 et[256];
     const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
     {
@@ -1597,6 +1599,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (!single_mode(n, a.N)) return;
     const uint8_t *in = raw + a.raw_off[b];
     uint8_t *out = enc + a.enc_off[b];
+    if (skip_ring && x1_enc_ok(in, out, n)) return;
     const bool vec_out = (((uintptr_t)out) & 15) == 0;
     uint32_t X = RANS_L << 8;  // x << 8 | a free low byte (see k_enc_xn)
     uint32_t xmin = 0xFFFFFFFFu;
@@ -1752,6 +1755,176 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 }
 
 
+
+// ----------------------------------------------------------------------
+// x1 encode with k_enc_xn's output path (encode_single, rans.rs:354-366, for
+// record batches with a shared table): two steps' bits paired into a 64-bit
+// accumulator whose low dword goes to slot nw of a per-lane LDS ring
+// ([slot][lane], conflict-free) every pair, branch-free. The record's place is
+// known before it is encoded, so the bytes go straight to it, in output units
+// of F = ERS / 2 dwords aligned to F * 4 bytes of the absolute address: output
+// dword d lives in ring slot (d + oal) mod ERS (oal = the record's dword offset
+// in its first unit), so a unit is always ring rows 0..F-1 or F..2F-1. At every
+// 16-symbol boundary a lane whose current unit is complete stores it (the
+// record's first unit only from its start). Input as k_enc_x1_fast: 64-B
+// blocks of the absolute address, the block below in flight.
+// Records this kernel takes: x1_enc_ok (16-B aligned input and output);
+// k_enc_x1_fast codes the others.
+// ----------------------------------------------------------------------
+__device__ __forceinline__ bool x1_enc_ok(const uint8_t *in, const uint8_t *out, uint64_t n) {
+    return ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0 && n < (1ull << 31);
+}
+
+#ifndef ZR_X1EW
+#define ZR_X1EW 256
+#define ZR_X1ERS 32
+#endif
+constexpr uint32_t X1EW = ZR_X1EW, X1ERS = ZR_X1ERS;  // records per workgroup, ring slots per lane
+
+template <uint32_t EW, uint32_t ERS>
+__global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t *enc, KArgs a) {
+    constexpr uint32_t F = ERS / 2;             // dwords per output unit
+    constexpr uint32_t ROW = EW * 4;            // ring row bytes
+    constexpr uint32_t RING_BYTES = ERS * ROW;  // a power of two
+    static_assert(ERS >= F + 9, "a tile adds up to 8 dwords to at most F - 1 pending and one partial");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16];
+    const uint32_t *ring = reinterpret_cast<const uint32_t *>(lds);
+    uint4 *et = reinterpret_cast<uint4 *>(lds + RING_BYTES);
+    const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t v = tid; v < 256; v += EW) {  // the k_enc_xn table layout
+        const uint32_t f = T->freq[v];
+        const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
+        et[v] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
+                           (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x * EW + tid;
+    if (b >= a.B) return;
+    const uint64_t n64 = a.len[b];
+    if (!single_mode(n64, a.N)) return;
+    const uint8_t *in = raw + a.raw_off[b];
+    uint8_t *out = enc + a.enc_off[b];
+    if (!x1_enc_ok(in, out, n64)) return;  // k_enc_x1_fast's
+    const uint32_t n = (uint32_t)n64;
+    uint32_t X = RANS_L << 8;
+    uint32_t xmin = 0xFFFFFFFFu;
+    uint64_t acc = 0;   // pending output bits (emission order from bit 0)
+    uint32_t nacc = 0;  // valid bits in acc, < 32 after every push
+    const uint32_t oal = (uint32_t)(((uintptr_t)out) >> 2) & (F - 1);  // (a multiple of 4)
+    uint32_t ra = tid * 4 + oal * ROW;  // + ROW * dwords completed, wrapped by one AND on use
+    uint32_t nw32 = 0;                  // 32 * dwords completed
+    uint32_t nfl = 0;                   // dwords stored
+    auto step = [&](const uint4 e, uint32_t &nb) -> uint32_t {  // see k_enc_xn
+        xmin = min(xmin, e.x);
+        const uint32_t xh = X >> 16;
+        nb = xh > (e.x >> 16) ? 16u : (xh > (e.x & 0xFFFFu) ? 8u : 0u);
+        const uint32_t bits = __builtin_amdgcn_ubfe(X, 8, nb);
+        const uint32_t Y = X >> nb;
+        const uint32_t q = __umulhi(Y & ~0xFFu, e.z) >> (e.w >> 24);
+        X = __umul24(q, e.w) + Y + e.y;
+        return bits;
+    };
+    auto push2 = [&](uint32_t bA, uint32_t nbA, uint32_t bB, uint32_t nbB) {
+        const uint32_t cpair = bA | (bB << nbA);
+        acc |= (uint64_t)cpair << nacc;
+        nacc += nbA + nbB;
+        *reinterpret_cast<uint32_t *>(lds + (ra & (RING_BYTES - 1))) = (uint32_t)acc;
+        const uint32_t t32 = nacc & 32;
+        ra += t32 * (ROW / 32);
+        nw32 += t32;
+        acc >>= t32;
+        nacc &= 31;
+    };
+    // store every complete unit (one per call but for the record's first, which
+    // can be short). The unit of dword nfl ends at ue; its first byte is
+    // out + 4 * (ue - F), i.e. out - 4 * oal for the record's first unit
+    auto flush = [&]() {
+        const uint32_t nw = nw32 >> 5;
+        for (;;) {
+            const uint32_t ue = ((nfl + oal) | (F - 1)) + 1 - oal;
+            if (nw < ue) break;
+            const uint32_t *r = ring + (((nfl + oal) & F) * EW) + tid;  // rows 0.. or F..
+            uint8_t *d = out + 4 * ((int64_t)ue - (int64_t)F);
+#pragma unroll
+            for (uint32_t qd = 0; qd < F / 4; qd++)
+                if (ue >= F || 4 * qd >= oal)
+                    reinterpret_cast<x4u *>(d)[qd] =
+                        x4u{r[(4 * qd) * EW], r[(4 * qd + 1) * EW], r[(4 * qd + 2) * EW], r[(4 * qd + 3) * EW]};
+            nfl = ue;
+        }
+    };
+    const uint32_t full = n & ~15u;
+    // the ragged top (< 16 symbols), one step at a time
+    for (uint32_t i = n; i > full;) {
+        uint32_t nb;
+        const uint32_t bits = step(et[in[--i]], nb);
+        push2(bits, nb, 0u, 0u);
+    }
+    flush();
+    if (full) {
+        int64_t c = (int64_t)(full >> 4) - 1;
+        const uint8_t *blk = in + 16 * c - (((uintptr_t)(in + 16 * c)) & 63);  // the top chunk's block
+        const x4u *cb = reinterpret_cast<const x4u *>(blk);
+        x4u w0 = cb[0], w1 = cb[1], w2 = cb[2], w3 = cb[3];
+        const x4u z = {0, 0, 0, 0};
+        const bool more = blk > in;  // the block below holds record bytes
+        x4u m0 = more ? cb[-4] : z, m1 = more ? cb[-3] : z, m2 = more ? cb[-2] : z, m3 = more ? cb[-1] : z;
+        auto enc16 = [&](const x4u wv) __attribute__((always_inline)) {
+#pragma unroll
+            for (int g = 3; g >= 0; g--) {
+                const uint32_t w = wv[g];
+                const uint4 e3 = et[w >> 24], e2 = et[(w >> 16) & 0xFF], e1 = et[(w >> 8) & 0xFF], e0 = et[w & 0xFF];
+                uint32_t n3, n2, n1, n0;
+                const uint32_t b3 = step(e3, n3);
+                const uint32_t b2 = step(e2, n2);
+                push2(b3, n3, b2, n2);
+                const uint32_t b1 = step(e1, n1);
+                const uint32_t b0 = step(e0, n0);
+                push2(b1, n1, b0, n0);
+            }
+            flush();
+        };
+        {  // the top block from chunk c's place p down (chunk c - p + k at place k)
+            const uint32_t p = (uint32_t)((((uintptr_t)in) >> 4) + (uint64_t)c) & 3;
+            const int64_t c0 = c - (int64_t)p;
+            if (p >= 3) enc16(w3);
+            if (p >= 2 && c0 + 2 >= 0) enc16(w2);
+            if (p >= 1 && c0 + 1 >= 0) enc16(w1);
+            if (c0 >= 0) enc16(w0);
+            c = c0 - 1;
+        }
+        while (c >= 0) {  // whole blocks below (chunk c at the block's top)
+            w0 = m0;
+            w1 = m1;
+            w2 = m2;
+            w3 = m3;
+            cb -= 4;
+            if (reinterpret_cast<const uint8_t *>(cb) > in) {
+                m0 = cb[-4];
+                m1 = cb[-3];
+                m2 = cb[-2];
+                m3 = cb[-1];
+            }
+            enc16(w3);
+            if (c >= 1) enc16(w2);
+            if (c >= 2) enc16(w1);
+            if (c >= 3) enc16(w0);
+            c -= 4;
+        }
+    }
+    // drain: the complete dwords not yet stored, the partial dword's whole bytes,
+    // then the u64 state (rans.rs:362-364)
+    const uint32_t nw = nw32 >> 5;
+    for (uint32_t i = nfl; i < nw; i++)
+        *reinterpret_cast<uint32_t *>(out + 4 * (size_t)i) = ring[((i + oal) & (ERS - 1)) * EW + tid];
+    size_t nout = 4 * (size_t)nw;
+    for (uint32_t t = 0; t < nacc / 8; t++) out[nout + t] = (uint8_t)(acc >> (8 * t));
+    nout += nacc / 8;
+    for (int t = 0; t < 8; t++) out[nout + t] = (uint8_t)((uint64_t)(X >> 8) >> (8 * t));
+    a.status[b] = (xmin == 0 && n) ? ZR_INVALID_INPUT : ZR_OK;  // "Symbol {} not in frequency table"
+    a.enc_len[b] = nout + 8;
+}
 
 // per-lane x1 decode straight from global memory, 64-bit state (the fallback
 // of k_dec_x1_ring for non-standard states and single-symbol/empty tables)
@@ -2449,7 +2622,14 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
     timer_begin("rans_encode_x1", s);
     if (!(bt->min_len >= a.N && a.N > 1)) {  // some buffer may take the x1 layout
         if (a.table_stride == 0) {
-            hipLaunchKernelGGL(k_enc_x1_fast, dim3((uint32_t)ceil_div(a.B, 256)), dim3(256), 0, s, raw, enc, a, w);
+#ifndef ZR_X1_NORING
+            // k_enc_x1_ring takes the records x1_enc_ok admits, k_enc_x1_fast the rest
+            hipLaunchKernelGGL((k_enc_x1_ring<X1EW, X1ERS>), dim3((uint32_t)ceil_div(a.B, X1EW)), dim3(X1EW), 0, s, raw,
+                               enc, a);
+            hipLaunchKernelGGL(k_enc_x1_fast, dim3((uint32_t)ceil_div(a.B, 256)), dim3(256), 0, s, raw, enc, a, 1);
+#else
+            hipLaunchKernelGGL(k_enc_x1_fast, dim3((uint32_t)ceil_div(a.B, 256)), dim3(256), 0, s, raw, enc, a, 0);
+#endif
         } else {
             hipLaunchKernelGGL(k_enc_x1_generic, dim3((uint32_t)ceil_div(a.B, 64)), dim3(64), 0, s, raw, a, w);
             hipLaunchKernelGGL(k_enc_x1_compact, dim3(a.B), dim3(64), 0, s, enc, a, w);
