@@ -1061,7 +1061,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         const uint32_t nunit = (wl + 15) / 16;
         for (uint32_t u = tid; u < nunit; u += 256) {
             const uint64_t q0 = win + 16 * (uint64_t)u;  // image offset of the unit
-            uint8_t *dst = reinterpret_cast<uint8_t *>(ua0 + q0);
+            // (pointer arithmetic from dbase, not an integer cast: a flat store
+            // counts in lgkmcnt, so the LDS waits and barriers after it would
+            // wait for the store itself)
+            uint8_t *dst = dbase + (int64_t)(ua0 + q0 - (uintptr_t)dbase);
             if (q0 >= lo && q0 + 16 <= span) {
                 // non-temporal: the encoded streams do not linger dirty in the XCD L2s
                 // (same-box A/B: the decode that reads them 0.200 -> 0.180 ms, the
@@ -1342,8 +1345,9 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // prologue: the 64-B segment holding the last stream byte and the one below
     const uintptr_t g1 = (pend - 1) & ~(uintptr_t)63;
     {
-        const v4u *p1 = reinterpret_cast<const v4u *>(clampa(g1));
-        const v4u *p0 = reinterpret_cast<const v4u *>(clampa(g1 - 64));
+        // (addresses rebased on e: global loads, not flat)
+        const v4u *p1 = reinterpret_cast<const v4u *>(e + (int64_t)(clampa(g1) - (uintptr_t)e));
+        const v4u *p0 = reinterpret_cast<const v4u *>(e + (int64_t)(clampa(g1 - 64) - (uintptr_t)e));
         const v4u a0 = p1[0], a1 = p1[1], a2 = p1[2], a3 = p1[3];
         const v4u b0 = p0[0], b1 = p0[1], b2 = p0[2], b3 = p0[3];
         put_seg((uint32_t)g1, a0, a1, a2, a3);
@@ -2185,8 +2189,9 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
     // prologue: the 64-B segment holding the record's last stream byte and the one below
     const uintptr_t g1 = (pend - 1) & ~(uintptr_t)63;
     {
-        const v4u *p1 = reinterpret_cast<const v4u *>(fast ? clampa(g1) : dummy);
-        const v4u *p0 = reinterpret_cast<const v4u *>(fast ? clampa(g1 - 64) : dummy);
+        // (addresses rebased on e: global loads, not flat)
+        const v4u *p1 = reinterpret_cast<const v4u *>(e + (int64_t)((fast ? clampa(g1) : dummy) - (uintptr_t)e));
+        const v4u *p0 = reinterpret_cast<const v4u *>(e + (int64_t)((fast ? clampa(g1 - 64) : dummy) - (uintptr_t)e));
         const v4u a0 = p1[0], a1 = p1[1], a2 = p1[2], a3 = p1[3];
         const v4u b0 = p0[0], b1 = p0[1], b2 = p0[2], b3 = p0[3];
         put_seg((uint32_t)g1, a0, a1, a2, a3);
