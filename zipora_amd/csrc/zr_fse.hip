@@ -429,11 +429,11 @@ __global__ __launch_bounds__(256) void k_fse_compact(FseEncArgs a, uint8_t *out,
             v.y = (uint32_t)((((uint64_t)w2 << 32) | w1) >> r);
             v.z = (uint32_t)((((uint64_t)w3 << 32) | w2) >> r);
             v.w = (uint32_t)((((uint64_t)w4 << 32) | w3) >> r);
-            *reinterpret_cast<uint4 *>(ua) = v;
+            *reinterpret_cast<uint4 *>(wd + o) = v;  // (rebased on wd: a global, not flat, store)
         } else {
             for (int t = 0; t < 16; t++) {
                 const int64_t p = o + t;
-                if (p >= 0 && (uint64_t)p < W) reinterpret_cast<uint8_t *>(ua)[t] = src[p];
+                if (p >= 0 && (uint64_t)p < W) wd[p] = src[p];
             }
         }
     }
