@@ -11,7 +11,7 @@ O=gpurun_out/prof_$R
 mkdir -p $O/summary
 B="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-path"
 BP="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-path"
-K="--kernel-include-regex k_dec_xn_fast|k_enc_xn|k_enc_compact|k_hist|k_fse_dec|k_fse_enc|k_copy16|k_enc_x1_fast|k_dec_x1_fast|k_dec_x1_ring|k_hist_small"
+K="--kernel-include-regex k_dec_xn_fast|k_enc_xn|k_enc_compact|k_hist|k_fse_dec|k_fse_enc|k_copy16|k_enc_x1_fast|k_enc_x1_ring|k_dec_x1_fast|k_dec_x1_ring|k_hist_small"
 # 1. rANS (headline) kernel trace + stats, default bench command
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rans -o rans -- $B > $O/rans_bench.log 2>&1
 # 2. HBM traffic, one counter group per pass
