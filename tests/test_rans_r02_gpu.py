@@ -470,3 +470,70 @@ def test_shared_table_exchange_two_ranks_on_device():
         p.join(timeout=30)
         assert p.exitcode == 0
     assert all(ok for _, ok in res)
+
+
+def test_wide_decode_errors_in_later_workgroups(zr, oracle):
+    """The 1024-lane decoder with its fused header (no k_dec_hdr): workgroup 0
+    of a buffer writes the first status and publishes the call's epoch, and an
+    error found by a later workgroup waits for it, so errors anywhere in a
+    buffer survive. Corrupted buffers (lengths moved between two streams of the
+    third workgroup, a changed state, a flipped stream bit, a truncated buffer,
+    a total over enc_len) decode error-for-error and byte-for-byte like the
+    oracle (rans.rs:555-651), over a status array pre-filled with garbage."""
+    import random
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    N, n, B = 4096, 1 << 18, 33  # 33 x 4096 streams > 2^16: the 1024-lane shape
+    datas = [zr.synth("t" if b % 2 else "u", n, seed=900 + b) for b in range(B)]
+    bt = RansDeviceBatch([n] * B, N, shared_table=False)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    tabs = [oracle.rans_table(oracle.histogram(d)) for d in datas]
+    host = bytearray(enc.cpu().numpy().tobytes())
+    enc_len = bt.enc_len.cpu().tolist()
+    rnd = random.Random(17)
+
+    def u32(buf, o):
+        return int.from_bytes(buf[o:o + 4], "little")
+
+    for b in range(1, B, 2):
+        o, L = bt.enc_off_host[b], enc_len[b]
+        kind = (b // 2) % 5
+        if kind == 0:  # 9 bytes of stream s moved to stream s+1 (same total)
+            s = rnd.randrange(2048, 3072)
+            ls, ls1 = o + 8 * N + 4 * s, o + 8 * N + 4 * (s + 1)
+            host[ls:ls + 4] = (u32(host, ls) - 9).to_bytes(4, "little")
+            host[ls1:ls1 + 4] = (u32(host, ls1) + 9).to_bytes(4, "little")
+        elif kind == 1:  # a state in [2^16, 2^24) changed
+            s = rnd.randrange(1024, N)
+            host[o + 8 * s:o + 8 * s + 8] = (0x10000 + rnd.randrange(1 << 20)).to_bytes(8, "little")
+        elif kind == 2:  # a flipped bit in the stream area
+            i = o + 12 * N + rnd.randrange(L - 12 * N)
+            host[i] ^= 1 << rnd.randrange(8)
+        elif kind == 3:  # truncated: the last stream is short
+            enc_len[b] = L - rnd.randrange(1, 40)
+        else:  # a length past enc_len ("Invalid stream data length")
+            s = rnd.randrange(N)
+            ls = o + 8 * N + 4 * s
+            host[ls:ls + 4] = (u32(host, ls) + 100000).to_bytes(4, "little")
+    enc.copy_(torch.frombuffer(host, dtype=torch.uint8).cuda())
+    bt.enc_len.copy_(torch.tensor(enc_len, dtype=torch.int64))
+    bt.status.fill_(-3)
+    out = bt.new_raw()
+    bt.decode(enc, out)
+    torch.cuda.synchronize()
+    st = bt.statuses()
+    for b in range(B):
+        o = bt.enc_off_host[b]
+        try:
+            ref = oracle.rans_decode(tabs[b], N, bytes(host[o:o + enc_len[b]]), n)
+        except oracle.OracleError:
+            ref = None
+        if ref is None:
+            assert st[b] != 0, f"buffer {b}: the oracle errs, the GPU reports ok"
+        else:
+            assert st[b] == 0, f"buffer {b}: the oracle decodes, GPU status {st[b]}"
+            assert bt.raw_of(out, b) == ref, f"buffer {b}"
