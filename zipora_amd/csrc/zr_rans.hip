@@ -1226,6 +1226,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     };
     // blo: the bytes of the buffer's streams below this workgroup's first one
     uint64_t blo;
+    uint32_t own_len = 0;  // (epoch mode: this lane's stream length, read with the others)
     if (epoch) {
         // min_header_size (rans.rs:563-568), then "Invalid stream data length"
         // (rans.rs:608-610), before any stream read
@@ -1237,6 +1238,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
                 const uint32_t v = stream_len(i);
                 tot += v;
                 lo += i < first ? v : 0u;
+                own_len = i == first + tid ? v : own_len;
             }
         }
         lo = wave_sum(lo);
@@ -1288,7 +1290,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     const uint32_t kind = T->kind;
     const uint32_t s = blkF * FW + tid;
     const bool active = s < N;
-    const uint32_t L = active ? stream_len(s) : 0;
+    const uint32_t L = !active ? 0u : epoch ? own_len : stream_len(s);
     const unsigned long long inc = wave_incl_scan(L);
     const int wv = tid >> 6;
     if ((tid & 63) == 63) sh[wv] = inc;
