@@ -176,3 +176,38 @@ def test_fse_device_full_size(zr, oracle):
         assert bytes(enc.cpu().numpy().tobytes()) == ref
         dec = dev.decompress(enc, n)
         assert torch.equal(dec, data)
+
+
+def test_fse_block_states_out_of_range_vs_oracle(zr, oracle):
+    """0xF6 streams whose block states were replaced by values outside the
+    decoder's bulk range [2^16, 2^48) (0, small, huge) or by random ones: the
+    device decode (status and bytes) equals the oracle's. Body layout
+    (fse.rs:1026-1044): F6 | nblocks u32 | size u32 x nblocks | bodies, each
+    body ending with its u64 state."""
+    import struct
+    data = zr.synth("z", 40 * 16384 + 777, seed=21)
+    par = bytearray(oracle.fse_compress(data, oracle.fse_config(parallel_blocks=4, block_size=16384)))
+    assert par[0] == 0xF6
+    nb = struct.unpack_from("<I", par, 1)[0]
+    sizes = struct.unpack_from(f"<{nb}I", par, 5)
+    ends, o = [], 5 + 4 * nb
+    for sz in sizes:
+        o += sz
+        ends.append(o)
+    rng = random.Random(77)
+    values = [0, 1, 5, 4095, 65535, 65536, (1 << 48) - 1, 1 << 48, (1 << 50) + 123, (1 << 64) - 1]
+    for it in range(12):
+        s = bytearray(par)
+        for b in rng.sample(range(nb), 6):
+            v = rng.choice(values) if it % 3 else rng.getrandbits(rng.choice([16, 32, 48, 64]))
+            struct.pack_into("<Q", s, ends[b] - 8, v)
+        s = bytes(s)
+        try:
+            want = oracle.fse_decompress(s)
+        except oracle.OracleError:
+            want = None
+        try:
+            got = zr.fse_decompress(s)
+        except zr.ZiporaError:
+            got = None
+        assert got == want, f"case {it}"
