@@ -172,10 +172,11 @@ __device__ void fse_build_table(uint32_t f, FseDTab *d, unsigned long long *sh, 
     d->shift[v] = shift;
     d->bias[v] = bias;
     d->cmpl[v] = cmpl;
-    // w: renorm threshold on the high word, (nf << 4) - 1 (x >= nf << 36 <=> x_hi > it),
-    // 0 for a symbol not in the table (encode_symbol -> None), | shift << 16
+    // w: shift | the renorm threshold on the high word << 16, (nf << 4) - 1 (x >= nf
+    // << 36 <=> x_hi > it), 0 for a symbol not in the table (encode_symbol -> None);
+    // the 64-bit shift reads w's low 6 bits and the compare w's high half in place
     d->enc[v] = make_uint4((uint32_t)rcp, (uint32_t)(rcp >> 32), bias | (cmpl << 16),
-                           (nf ? (nf << 4) - 1 : 0u) | (shift << 16));
+                           shift | ((nf ? (nf << 4) - 1 : 0u) << 16));
     if (v == 0) {
         d->status = ZR_OK;
         d->nsym = nsym;
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
     uint64_t x = 1;  // fse.rs:931
     bool err = false;
     auto step_e = [&](const uint4 e) {
-        const uint32_t thr = e.w & 0xFFFF;
+        const uint32_t thr = e.w >> 16;
         err |= (thr == 0);  // encode_symbol returns None (fse.rs:946-953)
         // renormalize_encode: x_max = ((RANS_L >> 12) << 32) * freq = freq << 36.
         // The word shift is branch-free (selects); only the 16-byte store of a
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
         const uint64_t t = (uint64_t)lo * e.y + __umulhi(lo, e.x);
         const uint64_t u = (uint64_t)hi * e.x + t;
         const uint64_t m = (uint64_t)hi * e.y + (u >> 32);
-        const uint64_t q = m >> (e.w >> 16);
+        const uint64_t q = m >> (e.w & 63);  // shift < 64
         // x + bias + q * cmpl (wrapping); q <= x < 2^48, so q_hi * cmpl fits 24 bits
         const uint32_t cm = e.z >> 16;
         const uint64_t xb = (((uint64_t)hi << 32) | lo) + (e.z & 0xFFFF);
