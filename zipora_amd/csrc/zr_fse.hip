@@ -303,7 +303,9 @@ __global__ __launch_bounds__(64) void k_fse_enc(FseEncArgs a) {
         // sum u wraps mod 2^64 exactly like the reference's (fse.rs:618-628)
         const uint64_t t = (uint64_t)lo * e.y + __umulhi(lo, e.x);
         const uint64_t u = (uint64_t)hi * e.x + t;
-        const uint64_t m = (uint64_t)hi * e.y + (u >> 32);
+        uint64_t uh;  // u >> 32 as an aligned register pair in one shift (not two moves)
+        asm("v_lshrrev_b64 %0, 32, %1" : "=v"(uh) : "v"(u));
+        const uint64_t m = (uint64_t)hi * e.y + uh;
         const uint64_t q = m >> (e.w & 63);  // shift < 64
         // x + bias + q * cmpl (wrapping); q <= x < 2^48, so q_hi * cmpl fits 24 bits
         const uint32_t cm = e.z >> 16;
