@@ -420,9 +420,12 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
     enc = bt.new_enc()
     out = bt.new_raw()
 
+    comm = zd.RcclComm(world, rank) if world > 1 else None  # the shared trained table over ranks
+
     def step():
         bt.histogram(raw)
-        zd.allreduce_histogram(bt.hist)
+        if comm is not None:
+            comm.allreduce_histogram(bt.hist)
         bt.tables_from_hist()
         bt.encode(raw, enc)
         bt.decode(enc, out)
@@ -530,10 +533,14 @@ def main():
     # lacks the consuming entry point, memset instead)
     consume = hasattr(L, "zr_rans_dtab_from_hist_consume_dev")
 
+    # the shared frequency table over ranks: the library's own RCCL communicator
+    # (zr_comm_*; the unique id travels over the torch process group, host side)
+    comm = zd.RcclComm(world, rank) if world > 1 else None
+
     def step():
         bt.histogram(raw, stream, zeroed=consume)
-        if world > 1:  # the shared frequency table: RCCL all-reduce of 256 counts
-            zd.allreduce_histogram(bt.hist)
+        if comm is not None:  # in-place u32 all-reduce of the 256 counts over xGMI
+            comm.allreduce_histogram(bt.hist, stream.cuda_stream)
         bt.tables_from_hist(stream, consume=consume)
         bt.encode(raw, enc, stream)
         bt.decode(enc, out, stream)
@@ -603,6 +610,8 @@ def main():
                                            sample_bytes=(16 << 20) if literal else None)
     if rank == 0:
         print(json.dumps(res), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -78,6 +78,13 @@ int32_t zr_rans_encode_adaptive(const uint8_t *in, size_t n, uint8_t *out, size_
  * freq 1..4096 and every x < 2^24, umulhi(x << 8, rcp) >> rsh == x / freq.
  * *mismatches receives the number of failures (0 expected). Synchronous. */
 int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches);
+/* Rans64Symbol::new(start, freq).fast_div(x) -> (x / freq, x % freq)
+ * (rans.rs:89-152, the pub symbol info of Rans64Encoder::get_symbol, rans.rs:423)
+ * for n dividends, computed on the device by the encoder's 24-bit reciprocal
+ * division for x < 2^24 (every state the coder holds) and by 64-bit division
+ * above. freq in 1..4096. Host arrays; synchronous. */
+int32_t zr_rans_symbol_fast_div(uint32_t start, uint32_t freq, const uint64_t *x, size_t n, uint64_t *q,
+                                uint64_t *r);
 
 /* ---- device-resident batch pipeline (the GPU hot path) ----
  * A batch is B independent buffers, each coded as one reference rANS stream
@@ -247,6 +254,30 @@ size_t zr_fse_decode_workspace_bytes(uint64_t max_blocks);
 int32_t zr_fse_decompress_dev(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
                               uint64_t max_blocks, uint64_t *out_len_dev, int32_t *status_dev,
                               void *workspace, size_t workspace_bytes, void *stream);
+
+/* ======================================================================
+ * Multi-GPU shared table on RCCL (xGMI) -- one process per GPU
+ * The reference trains one table on all of its data (RansBlobStore::train,
+ * blob_store/entropy.rs:212-219; AdaptiveRans64Encoder, rans.rs:708-714).
+ * Sharded over ranks, each rank counts its shard (zr_histogram_dev), the
+ * counts are summed over the ranks in place, and every rank builds the same
+ * table on its device (zr_rans_dtab_from_hist_dev). librccl is opened on the
+ * first zr_comm_* call (ZR_UNSUPPORTED if absent). The caller moves the
+ * unique id between its processes (ncclGetUniqueId/ncclCommInitRank contract).
+ * ====================================================================== */
+#define ZR_COMM_ID_BYTES 128
+typedef struct zr_comm zr_comm;
+/* rank 0 creates the id and shares it with the other ranks' processes */
+int32_t zr_comm_unique_id(uint8_t id[ZR_COMM_ID_BYTES]);
+/* collective over nranks processes; binds the calling thread's current device */
+int32_t zr_comm_init(const uint8_t id[ZR_COMM_ID_BYTES], int32_t nranks, int32_t rank, zr_comm **comm);
+/* in-place u32 SUM of n_bins device counters over the ranks (wraps mod 2^32 per
+ * bin, as the reference's u32 counts); stream-ordered */
+int32_t zr_histogram_allreduce_dev(zr_comm *comm, uint32_t *hist_dev, uint32_t n_bins, void *stream);
+/* broadcast n_tables device tables (zr_rans_dtab_bytes() each) from root:
+ * the alternative to re-building the table on every rank; stream-ordered */
+int32_t zr_table_broadcast_dev(zr_comm *comm, void *dtabs_dev, uint32_t n_tables, int32_t root, void *stream);
+int32_t zr_comm_destroy(zr_comm *comm);
 
 /* ======================================================================
  * Huffman order-0 -- src/entropy/huffman/{tree,encoder,decoder}.rs

@@ -2,7 +2,10 @@
 (round 2; SURVEY.md Appendix B holds B1-B14). Each vector's derivation is in
 the comment above it: the table the reference builds, then the coder state
 after every step that matters. They pin the CPU oracle (not gpu) and the HIP
-path through the C ABI (gpu) to bytes that neither of them produced.
+path through the C ABI (gpu) to bytes that neither of them produced -- except
+C4's two block bodies (words and final states), which are the oracle's output:
+C4's framing, block split, global table and raw tail are derived by hand below,
+its 2 x 100 coder steps are not (see the note at C4).
 
 Arithmetic is the reference's, in release mode (wrapping u64, Cargo.toml
 [profile.release]). rANS: L = 2^16, M = 4096, encode_symbol renormalises while
@@ -75,6 +78,10 @@ C3 = ("ab" * 50,
 # stored raw (len | FF | bytes, fse.rs:892-904).
 # Each coded block: len 100 | 0C | nsym 3 | (61, 0x562) (62, 0x54F) (63, 0x54F)
 # | words | state (the block bodies are 0x2E, 0x2E and 0x37 bytes).
+# NOT hand-derived: the two 16-byte word runs and the two final states below
+# are the oracle's output (100 coder steps each were not stepped by hand). An
+# independent re-derivation of fse.rs by the round-2 reviewer reproduced them,
+# so they pin framing + table by hand and the bodies by two restatements.
 C4_DATA = bytes(b"abc"[(7 * i) % 3] for i in range(250))
 C4 = ("f6" "03000000" "2e000000" "2e000000" "37000000"
       "64000000" "0c" "0300" "6162050000" "624f050000" "634f050000"

@@ -75,6 +75,12 @@ SIGNATURES = [
     ("zr_rans_adaptive_streams", ctypes.c_uint32, [c_sz]),
     ("zr_rans_encode_adaptive", ctypes.c_int32, [c_u8p, c_sz, c_u8p, c_sz, ctypes.POINTER(c_sz), c_u32p]),
     ("zr_rans_selftest_reciprocal", ctypes.c_int32, [c_u64p]),
+    ("zr_comm_unique_id", ctypes.c_int32, [c_u8p]),
+    ("zr_comm_init", ctypes.c_int32, [c_u8p, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(c_vp)]),
+    ("zr_histogram_allreduce_dev", ctypes.c_int32, [c_vp, c_vp, ctypes.c_uint32, c_vp]),
+    ("zr_table_broadcast_dev", ctypes.c_int32, [c_vp, c_vp, ctypes.c_uint32, ctypes.c_int32, c_vp]),
+    ("zr_comm_destroy", ctypes.c_int32, [c_vp]),
+    ("zr_rans_symbol_fast_div", ctypes.c_int32, [ctypes.c_uint32, ctypes.c_uint32, c_u64p, c_sz, c_u64p, c_u64p]),
     ("zr_device_alloc_count", ctypes.c_int32, [c_u64p]),
     ("zr_rans_dtab_bytes", c_sz, []),
     ("zr_rans_dtab_upload", ctypes.c_int32, [ctypes.POINTER(RansTable), ctypes.c_uint32, c_vp, c_vp]),

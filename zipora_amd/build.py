@@ -20,7 +20,8 @@ LIB_DIAG = os.path.join(PKG, "libzipora_amd_diag.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ZR_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["zr_api.cpp", "zr_rans.hip", "zr_fse.hip", "zr_huff.hip", "zr_pipe.cpp", "zr_compressor.hip"]
+SOURCES = ["zr_api.cpp", "zr_rans.hip", "zr_fse.hip", "zr_huff.hip", "zr_pipe.cpp", "zr_compressor.hip",
+           "zr_comm.cpp"]
 HEADERS = ["zr_internal.h", os.path.join("..", "..", "include", "zipora_amd.h")]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
           "-Wno-unused-function", "-Wno-unused-variable", "-munsafe-fp-atomics"]
@@ -58,7 +59,7 @@ def build(force=False, verbose=False, diag=False):
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, diag), srcs))
     if _newer(lib, objs) or force:
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs + ["-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")

@@ -1390,6 +1390,13 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
                                        : *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) +
                                                                              ((hi >> 6) & 0x3FFC));
         x = __umul24(ent >> 20, hi >> 20) + ((ent >> 8) & 0xFFF);
+        // sensitivity probes (diagnostic builds): 16 = two more VALU on the step's
+        // chain, 32 = two more VALU off it
+        if (ABL & 16) asm volatile("v_add_u32 %0, 0, %0\n\tv_add_u32 %0, 0, %0" : "+v"(x));
+        if (ABL & 32) {
+            uint32_t d0, d1;
+            asm volatile("v_mov_b32 %0, 0\n\tv_mov_b32 %1, 1" : "=v"(d0), "=v"(d1));
+        }
         return ent;
     };
     uint32_t sink = 0;
@@ -1432,8 +1439,9 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // tile boundary t, staging set (s0..s3) = the set of parity t & 1, pmine its
     // in-flight flag
     auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3, bool &pmine, bool pother) {
-        // every read of the previous tile was at or above pos - 4
-        bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        // every read of the previous tile was at or above pos - 4 (the no-refill
+        // ablation reads stale ring bytes on purpose: no fallback there)
+        bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if (t >= 2) {
             // wait for the loads of boundary t-2: younger are the 16 stores of tile
             // t-2, the 4 loads of boundary t-1 and the 16 stores of tile t-1 (every
@@ -1498,7 +1506,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         // ---- last tile (1..DT2 steps): every segment in flight lands first
         asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
                      "+v"(o2), "+v"(o3)::"memory");
-        bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if constexpr (PF) {
             if (pnd_o) land(o0, o1, o2, o3);
             if (pnd_e) land(e0, e1, e2, e3);
@@ -1515,7 +1523,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         for (uint32_t j = 0; j < nst; j++) {
             const uint64_t k = k0 + j;
             const bool live = k < c;
-            if (live) bad |= active && (int32_t)(pos8 - 32 - lov8()) < 0;
+            if (live) bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
             uint32_t h, l, sf;
             const uint32_t ent = step(readD(pos8), h, l, sf);
             pos8 = pos8 + 8 - sf;
@@ -2366,6 +2374,23 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
 // freq and 2^18 consecutive x; each thread walks 1024 x keeping the true
 // quotient incrementally (one hardware division per thread).
 // ======================================================================
+// Rans64Symbol::new(start, freq).fast_div(x) (rans.rs:89-152) on the device: the
+// encoder's own 24-bit reciprocal division (enc_div, every x < 2^24 the coder
+// can hold), the 64-bit quotient beyond that domain
+__global__ __launch_bounds__(256) void k_fast_div(uint32_t freq, const uint64_t *x, uint64_t n, uint64_t *q,
+                                                  uint64_t *r) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t v = x[i];
+    uint64_t qq;
+    if (v < (1ull << 24))
+        qq = enc_div((uint32_t)v, enc_rcp(freq), enc_rsh(freq));
+    else
+        qq = v / freq;
+    q[i] = qq;
+    r[i] = v - qq * freq;
+}
+
 __global__ __launch_bounds__(256) void k_rcp_selftest(unsigned long long *bad, uint32_t *first) {
     const uint32_t f = blockIdx.x / 64 + 1;
     const uint32_t x0 = (blockIdx.x % 64) * (1u << 18) + threadIdx.x * 1024;
@@ -2519,6 +2544,31 @@ int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches) {
     if ((st = L.sync())) return st;
     *mismatches = meta[0];
     return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_rans_symbol_fast_div(uint32_t start, uint32_t freq, const uint64_t *x, size_t n, uint64_t *q,
+                                uint64_t *r) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    (void)start;  // Rans64Symbol::fast_div reads only the frequency
+    if (n && (!x || !q || !r)) return set_error(ZR_INVALID_INPUT, "null argument");
+    if (freq == 0 || freq > TOTFREQ) return set_error(ZR_INVALID_INPUT, "frequency outside 1..4096");
+    if (n == 0) return ZR_OK;
+    if (n > (1u << 24)) return set_error(ZR_UNSUPPORTED, "more than 2^24 dividends per call");
+    CallLease L;
+    int32_t st = L.acquire();
+    if (st) return st;
+    void *d;
+    if ((st = L.get(2, 24 * n, &d))) return st;
+    uint64_t *dx = reinterpret_cast<uint64_t *>(d), *dq = dx + n, *dr = dq + n;
+    hipStream_t s = L.stream();
+    ZR_HIP(hipMemcpyAsync(dx, x, 8 * n, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_fast_div, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, s, freq, dx, (uint64_t)n, dq, dr);
+    ZR_HIP(hipGetLastError());
+    ZR_HIP(hipMemcpyAsync(q, dq, 8 * n, hipMemcpyDeviceToHost, s));
+    ZR_HIP(hipMemcpyAsync(r, dr, 8 * n, hipMemcpyDeviceToHost, s));
+    return L.sync();
     ZR_GUARD_END
 }
 
@@ -2693,6 +2743,11 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
                 case 4: kern = k_dec_xn_fast<1024, 4>; break;
                 case 7: kern = k_dec_xn_fast<1024, 7>; break;
                 case 8: kern = k_dec_xn_fast<1024, 8>; break;
+                case 5: kern = k_dec_xn_fast<1024, 5>; break;
+                case 16: kern = k_dec_xn_fast<1024, 16>; break;
+                case 32: kern = k_dec_xn_fast<1024, 32>; break;
+                case 21: kern = k_dec_xn_fast<1024, 21>; break;
+                case 37: kern = k_dec_xn_fast<1024, 37>; break;
                 default: break;
             }
 #else

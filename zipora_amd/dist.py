@@ -38,6 +38,70 @@ def allreduce_histogram(hist):
     return hist
 
 
+class RcclComm:
+    """The library's own RCCL communicator (zr_comm_*, zr_comm.cpp): what a
+    Rust host binding libzipora_amd.so uses for the shared table, with no
+    PyTorch in the data path. The 128-byte unique id is moved between the
+    processes by any host channel; `exchange_id` below uses torch.distributed's
+    object broadcast when a process group exists (world size 1: none needed)."""
+
+    def __init__(self, nranks=1, rank=0, unique_id=None):
+        import ctypes
+        from . import _lib
+        from .errors import check
+        self._L = _lib.load()
+        self._check = check
+        if unique_id is None:
+            unique_id = RcclComm.unique_id() if nranks == 1 else exchange_id(rank)
+        self.id = bytes(unique_id)
+        self.nranks, self.rank = int(nranks), int(rank)
+        idbuf = (ctypes.c_uint8 * 128).from_buffer_copy(self.id)
+        h = ctypes.c_void_p()
+        check(self._L.zr_comm_init(idbuf, self.nranks, self.rank, ctypes.byref(h)))
+        self._h = h
+
+    @staticmethod
+    def unique_id():
+        import ctypes
+        from . import _lib
+        from .errors import check
+        buf = (ctypes.c_uint8 * 128)()
+        check(_lib.load().zr_comm_unique_id(buf))
+        return bytes(buf)
+
+    def allreduce_histogram(self, hist, stream=None):
+        """In-place u32 SUM over the ranks of a device histogram (int32/uint32 tensor)."""
+        if stream is None:
+            stream = torch.cuda.current_stream(hist.device).cuda_stream
+        self._check(self._L.zr_histogram_allreduce_dev(self._h, hist.data_ptr(), hist.numel(), stream))
+        return hist
+
+    def broadcast_tables(self, tables, n_tables, root=0, stream=None):
+        if stream is None:
+            stream = torch.cuda.current_stream(tables.device).cuda_stream
+        self._check(self._L.zr_table_broadcast_dev(self._h, tables.data_ptr(), n_tables, root, stream))
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._check(self._L.zr_comm_destroy(h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def exchange_id(rank):
+    """Rank 0's RCCL unique id, delivered to every rank over the existing
+    torch.distributed process group (host objects only)."""
+    obj = [RcclComm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
 def max_over_ranks(seconds, device=None):
     """The bench contract's timing: the slowest rank's wall time."""
     t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)

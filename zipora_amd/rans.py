@@ -35,9 +35,23 @@ def _u8(data):
 
 
 class Rans64Symbol:
+    """Rans64Symbol::new(start, freq) (rans.rs:89-104)."""
+
     def __init__(self, start, freq):
         self.start = start
         self.freq = freq
+
+    def fast_div(self, x):
+        """Rans64Symbol::fast_div (rans.rs:137-152): (x / freq, x % freq), on the
+        device (the encoder's reciprocal division below 2^24). x: int or list."""
+        xs = [int(x)] if isinstance(x, int) else [int(v) for v in x]
+        n = len(xs)
+        xa = (ctypes.c_uint64 * max(1, n))(*xs)
+        qa = (ctypes.c_uint64 * max(1, n))()
+        ra = (ctypes.c_uint64 * max(1, n))()
+        check(_lib.load().zr_rans_symbol_fast_div(self.start, self.freq, xa, n, qa, ra))
+        res = [(qa[i], ra[i]) for i in range(n)]
+        return res[0] if isinstance(x, int) else res
 
 
 class Rans64Encoder:
