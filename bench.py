@@ -35,6 +35,8 @@ def parse():
     p.add_argument("--kind", default="u")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the configs[1]-literal / configs[2] / configs[4] sub-lines of the default run")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--workload", default="rans", choices=["rans", "fse", "o1", "blob"],
                    help="rans = BASELINE metric (configs[1]); fse = configs[2]; o1 = configs[3] "
@@ -164,9 +166,9 @@ def kernel_ms(L, name):
 
 def cpu_baseline_fse(host, bs, threads):
     """The oracle (C restatement of src/entropy/fse.rs, 'port'): FSE 0xF6
-    compress+decompress on bounded slices, slices spread over threads."""
+    compress+decompress on bounded 8 MiB slices, two legs: every allotted core
+    (slices spread over threads) and one thread."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import concurrent.futures as cf
     import oracle_ffi as O
     O.lib()
     sl = 8 << 20
@@ -180,10 +182,50 @@ def cpu_baseline_fse(host, bs, threads):
         return len(enc)
 
     dt, passes = _cpu_repeat(one, range(ns), threads)
+    dt1, p1 = _cpu_repeat(one, range(1), 1)
+    what = f"0xF6 stream (Some(8), {bs >> 10} KiB blocks), compress+decompress"
     return {"value": round(passes * ns * sl / 2**30 / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{passes} passes over {ns} x 8 MiB slices of the same Zipf workload, each an independent "
-                      f"0xF6 stream (Some(8), {bs >> 10} KiB blocks), compress+decompress, {threads} threads, "
-                      f"{dt:.2f} s wall"}
+                      f"{what}, {threads} threads, {dt:.2f} s wall",
+            "single_thread": {"value": round(p1 * sl / 2**30 / dt1, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                              "sample": f"{p1} passes over 1 x 8 MiB slice, {what}, {dt1:.2f} s wall"}}
+
+
+def fse_host_rates(L, torch, host, bs, reps=3):
+    """configs[2] starting and ending in host memory (north_star: the rate with the
+    H2D and D2H copies): zr_fse_compress / zr_fse_decompress on pinned host
+    buffers (the C ABI's host entry points: copy in, code on the device, copy out)."""
+    import ctypes
+    from zipora_amd import _lib as zl
+    n = len(host)
+    cfg = zl.FseConfig()
+    L.zr_fse_config_default(ctypes.byref(cfg))
+    cfg.parallel_blocks, cfg.block_size = 8, bs
+    pin = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    pin.copy_(torch.frombuffer(bytearray(host), dtype=torch.uint8))
+    cap = L.zr_fse_compress_bound(n, ctypes.byref(cfg))
+    penc = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+    pout = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    ol, dl = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    u8 = lambda t: ctypes.cast(t.data_ptr(), ctypes.POINTER(ctypes.c_uint8))  # noqa: E731
+    te = td = 0.0
+    for r in range(reps + 1):  # the first call grows the call context's buffers
+        t0 = time.perf_counter()
+        if L.zr_fse_compress(ctypes.byref(cfg), u8(pin), n, u8(penc), cap, ctypes.byref(ol)):
+            raise SystemExit("FSE host compress failed")
+        t1 = time.perf_counter()
+        if L.zr_fse_decompress(u8(penc), ol.value, u8(pout), n, ctypes.byref(dl)):
+            raise SystemExit("FSE host decompress failed")
+        t2 = time.perf_counter()
+        if r:
+            te += t1 - t0
+            td += t2 - t1
+    if dl.value != n or not torch.equal(pout, pin):
+        raise SystemExit("FSE host round trip mismatch")
+    return {"host_resident_gibps": round(n * reps / (te + td) / 2**30, 3),
+            "host_encode_gibps": round(n * reps / te / 2**30, 3),
+            "host_decode_gibps": round(n * reps / td / 2**30, 3),
+            "host_path": "zr_fse_compress/zr_fse_decompress, pinned host buffers, synchronous H2D + kernels + D2H"}
 
 
 def run_fse(args, torch, dist, world, rank, dev, zr, L):
@@ -230,6 +272,9 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
         "kernels_ms": kms, "kernels_ms_source": KMS_SOURCE,
         "compressed_bytes": clen, "ratio": round(clen / total, 5),
     }
+    del raw, enc, out
+    if rank == 0 and world == 1 and not args.no_host_path:
+        res.update(fse_host_rates(L, torch, host, bs))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_fse(host, bs, cpu_threads(args))
     return res
@@ -242,24 +287,38 @@ KMS_SOURCE = ("instrumented pass before the timed region (every kernel HIP-event
 
 
 COPY_GBS = None  # the achievable-copy ceiling, measured once per run
+COPY_NOTE = None
 
 
-def copy_ceiling(torch, dev, nbytes=256 << 20, reps=20):
-    """Device-to-device copy of 256 MiB (read + write bytes / time, GB/s): the
-    practical one-pass ceiling reported beside the 8 TB/s spec peak."""
-    global COPY_GBS
+def copy_ceiling(torch, dev, L, nbytes=256 << 20, reps=20):
+    """Device-to-device copy of 256 MiB by the library's 16-B-per-lane streaming
+    kernel (zr_memcpy_dev, four loads in flight per lane), read + write bytes /
+    time, the best of three grid sizes, timed with HIP events on the stream it
+    runs on: the practical one-pass ceiling reported beside the 8 TB/s spec peak."""
+    global COPY_GBS, COPY_NOTE
     if COPY_GBS is None:
         a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         b = torch.empty_like(a)
-        for _ in range(3):
-            b.copy_(a)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            b.copy_(a)
-        e1.record()
-        e1.synchronize()
-        COPY_GBS = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        st = torch.cuda.current_stream(dev)
+        best, best_g = 0.0, 0
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        if not hasattr(L, "zr_memcpy_dev"):  # (an older library in an A/B run: no ceiling)
+            COPY_GBS, COPY_NOTE = 0.0, "unmeasured"
+            return COPY_GBS
+        for g in (4 * cus, 8 * cus, 16 * cus):
+            for _ in range(3):
+                L.zr_memcpy_dev(b.data_ptr(), a.data_ptr(), nbytes, g, st.cuda_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(reps):
+                L.zr_memcpy_dev(b.data_ptr(), a.data_ptr(), nbytes, g, st.cuda_stream)
+            e1.record(st)
+            e1.synchronize()
+            gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+            if gbs > best:
+                best, best_g = gbs, g
+        COPY_GBS = best
+        COPY_NOTE = f"zr_memcpy_dev 256 MiB, 16 B/lane, grid {best_g} x 256, read+write bytes / time"
         del a, b
     return COPY_GBS
 
@@ -276,6 +335,7 @@ def _roofline(dom, dom_ms, bytes_of, traffic_wl, sym):
          "kernel": f"{sym[dom]} ({dom})", "bytes_per_launch": nbytes, "avg_launch_ms": round(dom_ms, 4)}
     if COPY_GBS:
         r["copy_ceiling"] = round(COPY_GBS, 1)
+        r["copy_ceiling_source"] = COPY_NOTE
         r["frac_of_copy"] = round(ach / COPY_GBS, 4)
     return r
 
@@ -357,7 +417,8 @@ def cpu_baseline_o1(host, threads):
 
 
 def cpu_baseline_blob(host, threads):
-    """Oracle rANS x1 per 1 KiB record with one shared table (RansCompressor-style)."""
+    """Oracle rANS x1 per 1 KiB record with one shared table (RansCompressor-style):
+    every allotted core over record groups, and one thread."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
     O.lib()
@@ -371,10 +432,15 @@ def cpu_baseline_blob(host, threads):
             assert O.rans_decode(t, 1, O.rans_encode(t, 1, d), 1024) == d
 
     dt, passes = _cpu_repeat(one, range((nrec + per - 1) // per), threads)
+    dt1, p1 = _cpu_repeat(one, range(1), 1)
     return {"value": round(passes * nrec * 1024 / 2**30 / dt, 4), "unit": "GiB/s", "cores": threads,
             "kind": "port",
             "sample": f"{passes} passes over {nrec} x 1 KiB records of the same batch, x1 encode+decode with "
-                      f"one shared table, {threads} threads, {dt:.2f} s wall"}
+                      f"one shared table, {threads} threads, {dt:.2f} s wall",
+            "single_thread": {"value": round(p1 * per * 1024 / 2**30 / dt1, 4), "unit": "GiB/s", "cores": 1,
+                              "kind": "port",
+                              "sample": f"{p1} passes over {per} x 1 KiB records, x1 encode+decode, shared table, "
+                                        f"{dt1:.2f} s wall"}}
 
 
 def run_o1(args, torch, dist, world, rank, dev, zr, L):
@@ -486,43 +552,16 @@ def host_pipe_rates(zr, bt, host, lens, N, steps):
             "host_decode_gibps": round(total * reps / td / 2**30, 3)}
 
 
-def main():
-    args = parse()
-    from zipora_amd import _lib as _zl
-    diag = _zl.diag_env()  # profiling ablations: garbage output, never a metric line
-    import torch
-    import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    import zipora_amd as zr
+def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=None, host_path=True,
+             cpu=True):
+    """configs[1]: rANS O0 encode+decode of B x n bytes per GPU, N-way streams,
+    one shared table (histogram -> [RCCL all-reduce] -> table -> encode -> decode)."""
     from zipora_amd import dist as zd
     from zipora_amd.device import RansDeviceBatch
-    L = zr.load()
-    L.zr_set_device(local)
-
-    copy_ceiling(torch, dev)
-    if args.workload in ("fse", "o1", "blob"):
-        fn = {"fse": run_fse, "o1": run_o1, "blob": run_blob}[args.workload]
-        res = fn(args, torch, dist, world, rank, dev, zr, L)
-        if diag:  # a diagnostic build or library override: kernel times only, never a metric line
-            res = {"diagnostic": diag, "kernels_ms": res.get("kernels_ms"), "ms_per_step": res["ms_per_step"]}
-        if rank == 0:
-            print(json.dumps(res), flush=True)
-        if world > 1:
-            dist.destroy_process_group()
-        return
-
-    B, n, N = args.buffers, args.buffer_mib << 20, args.streams
     total = B * n
-    host = zr.synth(args.kind, total, seed=0x9E3779B97F4A7C15 + rank)
-    raw = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+    if host is None:
+        host = zr.synth(args.kind, total, seed=0x9E3779B97F4A7C15 + rank)
+    raw = torch.frombuffer(bytearray(host[:total]), dtype=torch.uint8).to(dev)
     bt = RansDeviceBatch([n] * B, N, device=dev, shared_table=True)
     enc = bt.new_enc()
     out = bt.new_raw()
@@ -561,11 +600,10 @@ def main():
             raise SystemExit("decode mismatch in timed region")
     comp_bytes = int(bt.enc_len.sum().item())
     value = world * total * args.steps / dt / 2**30
+    if comm is not None:
+        comm.close()
     if diag:  # tools/*.sh read the kernel times; no metric from a diagnostic build
-        if rank == 0:
-            print(json.dumps({"diagnostic": diag, "kernels_ms": kms, "ms_per_step": round(dt / args.steps * 1e3, 4)}),
-                  flush=True)
-        return
+        return {"diagnostic": diag, "kernels_ms": kms, "ms_per_step": round(dt / args.steps * 1e3, 4)}
     literal = B == 1
     wl = "rans_literal" if literal else "rans"
     rans_bytes = {"rans_encode": total + comp_bytes, "rans_decode": comp_bytes + total,
@@ -602,16 +640,91 @@ def main():
         "compressed_bytes": comp_bytes,
         "ratio": round(comp_bytes / total, 5),
     }
-    if rank == 0 and world == 1 and not args.no_host_path:
-        res.update(host_pipe_rates(zr, bt, host, [n] * B, N, args.steps))
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and host_path and not args.no_host_path:
+        res.update(host_pipe_rates(zr, bt, host[:total], [n] * B, N, args.steps))
+    if rank == 0 and world == 1 and cpu and not args.no_cpu_baseline:
         # literal config: 16 MiB slices of the buffer, each its own x4096 stream set
         res["cpu_baseline"] = cpu_baseline(host, n, B, N, cpu_threads(args),
                                            sample_bytes=(16 << 20) if literal else None)
+    del raw, enc, out, bt
+    return res
+
+
+SECONDARY_KEYS = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "config", "roofline",
+                  "roofline_decode", "kernels_ms", "compressed_bytes", "ratio", "cpu_baseline",
+                  "host_resident_gibps", "host_encode_gibps", "host_decode_gibps")
+
+
+def secondary_lines(args, torch, dist, world, rank, dev, zr, L, host):
+    """The other BASELINE configs in the default run, each a
+    short run of its own workload: configs[1] as written (one 256 MiB buffer x
+    4096 streams), configs[2] (FSE, 64 KiB blocks), configs[4] (the 1 M x 1 KiB
+    record batch). Not part of `value`."""
+    import copy
+    out = {}
+
+    def sub(steps, warmup):
+        a = copy.copy(args)
+        a.steps, a.warmup = steps, warmup
+        return a
+
+    def slim(r):
+        return {k: r[k] for k in SECONDARY_KEYS if k in r}
+
+    out["rans_literal"] = slim(run_rans(sub(3, 1), torch, dist, world, rank, dev, zr, L, 1, 256 << 20, 4096,
+                                        host=host, host_path=False))
+    torch.cuda.empty_cache()
+    a = sub(3, 1)
+    a.fse_block_kib = 64
+    out["fse"] = slim(run_fse(a, torch, dist, world, rank, dev, zr, L))
+    torch.cuda.empty_cache()
+    a = sub(5, 2)
+    a.records = 1 << 20
+    out["blob"] = slim(run_blob(a, torch, dist, world, rank, dev, zr, L))
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    from zipora_amd import _lib as _zl
+    diag = _zl.diag_env()  # profiling ablations: garbage output, never a metric line
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import zipora_amd as zr
+    L = zr.load()
+    L.zr_set_device(local)
+
+    copy_ceiling(torch, dev, L)
+    if args.workload in ("fse", "o1", "blob"):
+        fn = {"fse": run_fse, "o1": run_o1, "blob": run_blob}[args.workload]
+        res = fn(args, torch, dist, world, rank, dev, zr, L)
+        if diag:  # a diagnostic build or library override: kernel times only, never a metric line
+            res = {"diagnostic": diag, "kernels_ms": res.get("kernels_ms"), "ms_per_step": res["ms_per_step"]}
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    B, n, N = args.buffers, args.buffer_mib << 20, args.streams
+    host = zr.synth(args.kind, B * n, seed=0x9E3779B97F4A7C15 + rank)
+    res = run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=diag, host=host)
+    headline = (B, n, N) == (64, 4 << 20, 4096)
+    if not diag and headline and world == 1 and not args.no_secondary:
+        torch.cuda.empty_cache()
+        res["secondary"] = secondary_lines(args, torch, dist, world, rank, dev, zr, L, host)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if comm is not None:
-        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

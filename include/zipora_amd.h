@@ -390,6 +390,9 @@ int32_t zr_free_dev(void *ptr);
 int32_t zr_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
 int32_t zr_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
 int32_t zr_memset_dev(void *dst, int value, size_t bytes, void *stream);
+/* device-to-device copy by a 16-B-per-lane streaming kernel (grid 0: 8 x CUs
+ * workgroups of 256): the achievable one-pass ceiling the bench reports */
+int32_t zr_memcpy_dev(void *dst, const void *src, size_t bytes, uint32_t grid, void *stream);
 int32_t zr_stream_sync(void *stream);
 
 /* ---- kernel timers: HIP events recorded around every launch of the named

@@ -106,14 +106,15 @@ def test_adaptive_select_variant_thresholds(zr):
 
 
 def test_stream_count_limit_checked_before_any_launch(zr):
-    """the 2^27-stream limit is refused up front (no kernel, no timer)."""
+    """the stream-count limit (2^26: a 32-row decoder tile spans < 2^31 B)
+    is refused up front (no kernel, no timer)."""
     from zipora_amd import _lib
     lib = zr.load()
     bt = _lib.RansBatch()
-    bt.n_buffers, bt.n_streams, bt.max_len = 1, 1 << 27, 1 << 28
+    bt.n_buffers, bt.n_streams, bt.max_len = 1, 1 << 26, 1 << 28
     for fn in (lib.zr_rans_encode_batch_dev, lib.zr_rans_decode_batch_dev):
         assert fn(ctypes.byref(bt), None, None, None, 0, None) == _lib.ZR_UNSUPPORTED
-        assert "2^27" in zr.last_error()
+        assert "2^26" in zr.last_error()
 
 
 def test_diagnostic_switches_are_tools_only():

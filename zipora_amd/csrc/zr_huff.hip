@@ -449,10 +449,13 @@ __device__ uint64_t seg_decode(const HuffDecArgs &a, uint64_t p, uint64_t lim, u
 // round r re-decodes the dirty segments, then moves every start to the end of
 // the previous segment and records in changed[r] whether any start moved.
 // Round r > 0 does nothing once round r-1 changed nothing (converged).
-__global__ __launch_bounds__(256) void k_huff_init(HuffDecArgs a, uint32_t nflags) {
+// k (non-zero): every code of the tree is k bits long, so the code boundaries
+// are exactly the multiples of k and the first guess is already right (a
+// fixed-length code never resynchronises from a wrong guess).
+__global__ __launch_bounds__(256) void k_huff_init(HuffDecArgs a, uint32_t nflags, uint32_t k) {
     const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (t < a.nseg) {
-        a.start[t] = t * HD_SEG;  // the guessed boundaries
+        a.start[t] = k ? (t * HD_SEG + k - 1) / k * k : t * HD_SEG;  // the guessed boundaries
         a.dirty[t] = 1;
     }
     if (t < nflags) a.changed[t] = 0;
@@ -481,21 +484,66 @@ __global__ __launch_bounds__(256) void k_huff_fix(HuffDecArgs a, uint32_t round)
     }
 }
 
-// After the parallel rounds: if the last round still moved a start, resolve
-// the rest in order on one thread (exact, O(stream) -- only for streams whose
-// wrong guesses did not resynchronise within the rounds).
-__global__ void k_huff_serial(HuffDecArgs a, uint32_t last) {
-    if (a.changed[last] == 0 || threadIdx.x != 0) return;
-    for (uint64_t t = 0; t < a.nseg; t++) {
-        if (t > 0 && a.end[t - 1] != a.start[t]) {
-            a.start[t] = a.end[t - 1];
-            a.dirty[t] = 1;
+// After the parallel rounds, if the last round still moved a start (a code set
+// whose wrong guesses do not resynchronise, e.g. a deserialized tree of
+// fixed-length codes of a length that does not divide the segment), the exact
+// starts come from a parallel resolve instead of an in-order walk:
+//   1. k_huff_map: for every segment t and every entry offset e < L (L = the
+//      longest code; the true start of t is the first code boundary >= t*SEG,
+//      so it is t*SEG + e for one such e) decode the segment and record the
+//      exit offset into segment t+1 (ME_END: the stream ended), nseg x L
+//      independent segment decodes;
+//   2. k_huff_compose: one workgroup composes those maps by a Hillis-Steele
+//      scan (log2 nseg levels), so C_t = f_t o ... o f_0 and segment t+1
+//      starts at (t+1)*SEG + C_t(0); starts that differ are marked dirty and
+//      one more k_huff_seg pass decodes them.
+// Both return at once when the rounds converged (the usual case).
+constexpr uint8_t ME_END = 0xFF;
+__global__ __launch_bounds__(256) void k_huff_map(HuffDecArgs a, uint32_t last, uint32_t L, uint8_t *map) {
+    if (a.changed[last] == 0) return;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.nseg * L) return;
+    const uint64_t t = i / L, e = i % L;
+    const uint64_t p = t * HD_SEG + e;
+    uint8_t r = ME_END;
+    if (p < a.B) {
+        uint64_t pe;
+        seg_decode<false>(a, p, min((t + 1) * HD_SEG, a.B), &pe, 0);
+        if (pe < a.B) r = (uint8_t)(pe - (t + 1) * HD_SEG);  // < L: a code started below the limit
+    }
+    map[i] = r;
+}
+
+__global__ __launch_bounds__(1024) void k_huff_compose(HuffDecArgs a, uint32_t last, uint32_t L, uint8_t *m0,
+                                                       uint8_t *m1) {
+    if (a.changed[last] == 0) return;
+    const uint64_t tot = a.nseg * L;
+    uint8_t *src = m0, *dst = m1;
+    for (uint64_t d = 1; d < a.nseg; d <<= 1) {
+        for (uint64_t i = threadIdx.x; i < tot; i += 1024) {
+            const uint64_t t = i / L, e = i % L;
+            uint8_t v = src[i];
+            if (t >= d) {  // C_t o C_{t-d}: first the lower segments' composite
+                const uint8_t u = src[(t - d) * L + e];
+                v = u == ME_END ? ME_END : src[t * L + u];
+            }
+            dst[i] = v;
         }
-        if (a.dirty[t]) {
-            uint64_t pe;
-            a.cnt[t] = seg_decode<false>(a, a.start[t], min((t + 1) * HD_SEG, a.B), &pe, 0);
-            a.end[t] = pe;
-            a.dirty[t] = 0;
+        __threadfence_block();
+        __syncthreads();
+        uint8_t *x = src;
+        src = dst;
+        dst = x;
+    }
+    for (uint64_t t = threadIdx.x; t < a.nseg; t += 1024) {
+        uint64_t st = 0;
+        if (t > 0) {
+            const uint8_t o = src[(t - 1) * L];  // C_{t-1}(0)
+            st = o == ME_END ? a.B : t * HD_SEG + o;
+        }
+        if (st != a.start[t]) {
+            a.start[t] = st;
+            a.dirty[t] = 1;
         }
     }
 }
@@ -692,7 +740,7 @@ size_t zr_huff_workspace_bytes(size_t n, size_t in_len) {
     const uint64_t B = (uint64_t)in_len * 8;
     const uint64_t nseg = std::max<uint64_t>(1, ceil_div(B, HD_SEG));
     const uint64_t dec = 4096 + round_up(in_len + 64, 256) + 3 * round_up(8 * nseg, 256) + round_up(nseg, 256) +
-                         round_up(4ull * 256 * 256, 256);
+                         round_up(4ull * 256 * 256, 256) + 2 * round_up(64 * nseg, 256);
     return (size_t)std::max(enc, dec);
 }
 
@@ -778,6 +826,10 @@ int32_t zr_huff_decode_dev(const zr_huff_tree *t, const uint8_t *in, size_t in_l
     a.dirty = w;
     w += round_up(nseg, 256);
     uint32_t *dlut = reinterpret_cast<uint32_t *>(w);
+    w += round_up(4ull * 256 * 256, 256);
+    uint8_t *map0 = w;  // the resolve's segment maps (nseg x L, L <= 64), ping-pong
+    w += round_up(64 * nseg, 256);
+    uint8_t *map1 = w;
     a.lut = dlut;
     a.changed = flag;
     a.out = out;
@@ -791,14 +843,33 @@ int32_t zr_huff_decode_dev(const zr_huff_tree *t, const uint8_t *in, size_t in_l
     ZR_HIP(hipLaunchHostFunc(
         s, [](void *p) { delete static_cast<std::vector<uint32_t> *>(p); }, held));
     const uint32_t g = (uint32_t)ceil_div(nseg, 256);
-    constexpr uint32_t ROUNDS = 4;  // chain and fixed-length codes settle in 1-2
-    hipLaunchKernelGGL(k_huff_init, dim3(g), dim3(256), 0, s, a, ROUNDS);
+    // chain codes resynchronise at their first 1 bit (every code but the
+    // all-zero one ends in a 1, tree.rs:187-208), fixed-length codes are seeded
+    // on their boundaries: both settle in round 0 or 1
+    constexpr uint32_t ROUNDS = 4;
+    uint32_t kfix = 0;
+    {
+        uint32_t lo = 64, hi = 0;
+        for (int v = 0; v < 256; v++)
+            if (t->code_len[v]) {
+                lo = std::min<uint32_t>(lo, t->code_len[v]);
+                hi = std::max<uint32_t>(hi, t->code_len[v]);
+            }
+        if (lo == hi) kfix = hi;
+    }
+    const uint32_t L = std::max<uint32_t>(1, std::min<uint32_t>(64, t->max_code_length));
+    hipLaunchKernelGGL(k_huff_init, dim3(g), dim3(256), 0, s, a, ROUNDS, kfix);
     timer_begin("huff_decode", s);
     for (uint32_t r = 0; r < ROUNDS; r++) {
         hipLaunchKernelGGL(k_huff_seg, dim3(g), dim3(256), 0, s, a, r);
         hipLaunchKernelGGL(k_huff_fix, dim3(g), dim3(256), 0, s, a, r);
     }
-    hipLaunchKernelGGL(k_huff_serial, dim3(1), dim3(64), 0, s, a, ROUNDS - 1);
+    // the parallel resolve (no-ops when round ROUNDS-1 moved nothing), then the
+    // re-decode of the segments it moved (k_huff_seg's round ROUNDS reads the
+    // same flag)
+    hipLaunchKernelGGL(k_huff_map, dim3((uint32_t)ceil_div(nseg * L, 256)), dim3(256), 0, s, a, ROUNDS - 1, L, map0);
+    hipLaunchKernelGGL(k_huff_compose, dim3(1), dim3(1024), 0, s, a, ROUNDS - 1, L, map0, map1);
+    hipLaunchKernelGGL(k_huff_seg, dim3(g), dim3(256), 0, s, a, ROUNDS);
     uint64_t *tot = reinterpret_cast<uint64_t *>(flag + 8);
     hipLaunchKernelGGL(k_huff_scan, dim3(1), dim3(256), 0, s, a.cnt, nseg, tot, (uint64_t *)nullptr,
                        (const int32_t *)nullptr);

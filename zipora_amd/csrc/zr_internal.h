@@ -13,6 +13,8 @@
 // ---------------------------------------------------------------------------
 namespace zr {
 int32_t set_error(int32_t code, const std::string &msg);
+// compute units of the current device (cached per device)
+uint32_t cu_count();
 void clear_error();
 
 #define ZR_HIP(expr)                                                                       \

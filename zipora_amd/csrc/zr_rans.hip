@@ -1416,7 +1416,16 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // records: the hardware drops it, so the stores need no exec mask.
     __amdgpu_buffer_rsrc_t orsrc = byte_rsrc(outb);
     const uint32_t voff = active ? tid : 0x80000000u;
-    const uint32_t nfull = (uint32_t)((cmax - 1) / DT2);  // tiles with k0 + DT2 < cmax
+    // packed stores (wide shape): lane 4q + r of a wave writes row r of streams
+    // 4q..4q+3; the transpose's byte selectors by the lane's place in its quad
+    const uint32_t voff_pk = (tid & ~3u) + (tid & 3u) * N;
+    const uint32_t psel1 = (tid & 2) ? 0x03020706u : 0x05040100u;  // 16-bit halves with lane ^ 2
+    const uint32_t psel2 = (tid & 1) ? 0x03070105u : 0x06020400u;  // bytes with lane ^ 1
+    // PF: DT2-step tiles with k0 + DT2 < cmax. Wide shape: TW-step tiles over
+    // the rows every stream of the buffer has (n / N of them), the rest in the
+    // tail loop
+    constexpr uint32_t TW = 32;
+    const uint32_t nfull = PF ? (uint32_t)((cmax - 1) / DT2) : (uint32_t)((n / N) / TW);
     auto lov8 = [&]() -> uint32_t { return PF ? lo8 : (uint32_t)lo64 << 3; };
     // a segment lands: the staging set becomes the 64 bytes below the resident ones
     auto land = [&](const v4u c0, const v4u c1, const v4u c2, const v4u c3) {
@@ -1494,13 +1503,95 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         }
     };
 
+    // ---- wide shape (1024 lanes per CU, 4 waves per SIMD): TW = 32-step tiles;
+    // a refill issued at boundary t lands at boundary t + 1 (32 steps, a few us,
+    // cover the load: one staging set, half the boundaries of 16-step tiles).
+    // Full waves over 4-aligned output pack the bytes of 4 steps into one dword
+    // store per lane: the quad's 4 x 4 bytes (lane r of the quad holds rows
+    // 4g..4g+3 of its stream) are transposed by two DPP lane swaps + v_perm,
+    // so lane 4q + r stores row 4g + r of streams 4q..4q+3: 8 dword stores per
+    // tile instead of 32 byte stores.
+    auto tile_w = [&](uint32_t t, bool pk) {
+        uint32_t D = readD(pos8);
+        orsrc = byte_rsrc(outb + (uint64_t)t * TW * N);
+        uint32_t row = 0, pk0 = 0;
+#pragma unroll
+        for (int j = 0; j < (int)TW / 2; j++) {
+            uint32_t hA, lA, sA, hB, lB, sB;
+            const uint32_t eA = step(D, hA, lA, sA);
+            const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
+            uint32_t used;
+            asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
+            pos8 -= used;
+            if (j + 1 < (int)TW / 2) D = readD(pos8);
+            if (ABL & 1) {
+                sink += eA ^ eB;
+            } else if (pk) {
+                if ((j & 1) == 0) {
+                    pk0 = __builtin_amdgcn_perm(eB, eA, 0x0c0c0400u);  // [eA, eB, 0, 0]
+                } else {
+                    uint32_t q = __builtin_amdgcn_perm(eB, eA, 0x04000c0cu) | pk0;  // rows 4g..4g+3
+                    uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0x4E, 0xF, 0xF, false);  // lane ^ 2
+                    q = __builtin_amdgcn_perm(x, q, psel1);
+                    x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+                    q = __builtin_amdgcn_perm(x, q, psel2);
+                    __builtin_amdgcn_raw_buffer_store_b32(q, orsrc, voff_pk, row - 2 * N, 0);
+                }
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, voff, row, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eB, orsrc, voff, row + N, 0);
+            }
+            row += 2 * N;
+        }
+    };
+    auto boundary_w = [&](uint32_t t, bool pk) {
+        bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        if (t >= 1) {
+            // the loads of boundary t - 1; younger: tile t-1's stores
+            if (ABL & 1)
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
+            else if (pk)
+                asm volatile("s_waitcnt vmcnt(8)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
+            else
+                asm volatile("s_waitcnt vmcnt(32)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
+            if (pnd) {
+                land(e0, e1, e2, e3);
+                pnd = false;
+            }
+        }
+        const bool issue = !(ABL & 4) && active && (int32_t)(pos8 - lov8()) <= 64 * 8;
+        const uintptr_t g = !issue ? dummy : clampa(lo64 - 64);
+        asm_load16(e0, g);
+        asm_load16_off<16>(e1, g);
+        asm_load16_off<32>(e2, g);
+        asm_load16_off<48>(e3, g);
+        pnd = issue;
+    };
+    if (!PF && wave_live) {
+        // packed stores: every lane of the wave a stream, 4-aligned rows
+        const bool pk = __builtin_amdgcn_readfirstlane(
+                            (uint32_t)(wave_all && (N & 3) == 0 && ((((uintptr_t)outb) & 3) == 0))) != 0;
+        if (pk) {
+            for (uint32_t t = 0; t < nfull; t++) {
+                boundary_w(t, true);
+                tile_w(t, true);
+            }
+        } else {
+            for (uint32_t t = 0; t < nfull; t++) {
+                boundary_w(t, false);
+                tile_w(t, false);
+            }
+        }
+    }
     if (wave_live) {
-        for (uint32_t t = 0; t < nfull; t += 2) {
-            boundary(t, e0, e1, e2, e3, pnd_e, pnd_o);
-            tile(t);
-            if (t + 1 < nfull) {
-                boundary(t + 1, o0, o1, o2, o3, pnd_o, pnd_e);
-                tile(t + 1);
+        if constexpr (PF) {
+            for (uint32_t t = 0; t < nfull; t += 2) {
+                boundary(t, e0, e1, e2, e3, pnd_e, pnd_o);
+                tile(t);
+                if (t + 1 < nfull) {
+                    boundary(t + 1, o0, o1, o2, o3, pnd_o, pnd_e);
+                    tile(t + 1);
+                }
             }
         }
         // ---- last tile (1..DT2 steps): every segment in flight lands first
@@ -1510,14 +1601,11 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         if constexpr (PF) {
             if (pnd_o) land(o0, o1, o2, o3);
             if (pnd_e) land(e0, e1, e2, e3);
-        } else if (pnd) {
-            if (ptile & 1)
-                land(o0, o1, o2, o3);
-            else
-                land(e0, e1, e2, e3);
+        } else if (pnd) {  // (wide shape: the one staging set)
+            land(e0, e1, e2, e3);
         }
         uint32_t pos_snap = pos8;
-        const uint64_t k0 = (uint64_t)nfull * DT2;
+        const uint64_t k0 = (uint64_t)nfull * (PF ? DT2 : TW);
         const uint32_t nst = (uint32_t)(cmax - k0);
         orsrc = byte_rsrc(outb + k0 * N);
         for (uint32_t j = 0; j < nst; j++) {
@@ -2487,18 +2575,6 @@ static uint64_t next_epoch() {
     return v;
 }
 
-// compute units of the current device (cached per device)
-static uint32_t cu_count() {
-    static int cached[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cached[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cached[dev] = n;
-    }
-    return (uint32_t)cached[dev];
-}
 
 static bool narrow_batch(const KArgs &a) { return (uint64_t)a.B * a.N <= (1u << 16); }
 
@@ -2633,8 +2709,8 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
     clear_error();
     if (!bt) return set_error(ZR_INVALID_INPUT, "null batch");
     if (bt->n_buffers == 0) return ZR_OK;
-    if (bt->n_streams >= (1u << 27))  // the decoder's limit: refuse what could not be decoded
-        return set_error(ZR_UNSUPPORTED, "more than 2^27 rANS streams");
+    if (bt->n_streams >= (1u << 26))  // the decoder's limit: refuse what could not be decoded
+        return set_error(ZR_UNSUPPORTED, "more than 2^26 rANS streams");
     KArgs a = kargs(bt);
     RansWork w;
     int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
@@ -2704,8 +2780,8 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
     clear_error();
     if (!bt) return set_error(ZR_INVALID_INPUT, "null batch");
     if (bt->n_buffers == 0) return ZR_OK;
-    if (bt->n_streams >= (1u << 27))  // a tile of DT2 output rows must span < 2^31 bytes
-        return set_error(ZR_UNSUPPORTED, "more than 2^27 rANS streams");
+    if (bt->n_streams >= (1u << 26))  // a tile of 32 output rows must span < 2^31 bytes
+        return set_error(ZR_UNSUPPORTED, "more than 2^26 rANS streams");
     KArgs a = kargs(bt);
     RansWork w;
     int32_t st = rans_carve(a.B, a.N, bt->max_len, ws, ws_bytes, &w);
