@@ -14,12 +14,21 @@
  * Buffers are caller-owned. Functions without the _dev suffix take HOST memory
  * and are synchronous (they return the codec status like the Rust Result).
  * They are thread-safe: each call leases a per-device call context (its own
- * non-blocking HIP stream and cached device buffers), synchronises only that
- * stream (never the device), and allocates nothing once the sizes it needs
- * have been seen (zr_device_alloc_count).
+ * non-blocking HIP stream and cached device buffers) and synchronises only that
+ * stream, never the device: a buffer that must grow is freed and re-allocated
+ * stream-ordered on the context's stream (hipFreeAsync / hipMallocAsync).
+ * Buffers up to 1 GiB stay cached in the context (nothing is allocated once the
+ * sizes a workload needs have been seen, zr_device_alloc_count); larger ones
+ * are returned when the call ends. zr_release_call_contexts() frees every idle
+ * context and trims the devices' memory pools.
  * Functions with the _dev suffix take DEVICE memory, are ordered on the given
  * HIP stream (hipStream_t passed as void*, NULL = default stream) and report
  * per-buffer status into a device int32 array; read it after synchronising.
+ * Graph capture: zr_rans_encode/decode_batch_dev, zr_histogram_dev and
+ * zr_rans_dtab_from_hist*_dev may be captured into a HIP graph (the decoder
+ * then takes its capture-safe path: no host-side call counter); the _dev calls
+ * that stage host data (zr_rans_dtab_upload, zr_huff_*_dev, zr_fse_*_dev,
+ * zr_ctx_huff_*_dev) return ZR_UNSUPPORTED on a capturing stream.
  */
 #ifndef ZIPORA_AMD_H
 #define ZIPORA_AMD_H
@@ -44,6 +53,9 @@ void zr_set_error_callback(zr_error_cb cb);    /* c_api.rs:22 */
 const char *zr_version(void);
 int32_t zr_device_count(int32_t *count);
 int32_t zr_set_device(int32_t device);         /* binds this host thread to a GPU */
+/* frees the idle call contexts of the host entry points (their cached device
+ * buffers and streams) and trims the default memory pools */
+int32_t zr_release_call_contexts(void);
 
 /* ======================================================================
  * rANS order-0 -- src/entropy/rans.rs

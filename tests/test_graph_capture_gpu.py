@@ -1,0 +1,82 @@
+"""HIP graph capture of the device pipeline: the histogram, table
+build, encode and decode captured once and replayed; each replay must produce
+the oracle's bytes, and a replay over a corrupted stream must report it (the
+decoder's capture-safe path keeps no host-side per-call state). The _dev calls
+that stage host data refuse a capturing stream."""
+import os
+import sys
+
+import pytest
+import torch
+
+import zipora_amd as zr
+from zipora_amd.device import RansDeviceBatch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import oracle_ffi as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def test_captured_step_replays_bit_exact():
+    lens = [300_000, 4096 * 40 + 17, 100]
+    N = 4096
+    ds = [zr.synth("u", n, seed=40 + i) for i, n in enumerate(lens)]
+    bt = RansDeviceBatch(lens, N, shared_table=True)
+    raw = bt.new_raw()
+    for b, d in enumerate(ds):
+        o = bt.raw_off_host[b]
+        raw[o:o + len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+    enc, out = bt.new_enc(), bt.new_raw()
+    side = torch.cuda.Stream()
+
+    def step(s):
+        bt.histogram(raw, s, zeroed=True)
+        bt.tables_from_hist(s, consume=True)
+        bt.encode(raw, enc, s)
+        bt.decode(enc, out, s)
+
+    with torch.cuda.stream(side):
+        step(side)  # eager warm-up (allocations, first-call setup)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        step(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    alld = b"".join(ds)
+    tab = O.rans_table(O.histogram(alld))
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        bt.raise_on_error()
+        for b, d in enumerate(ds):
+            assert bt.raw_of(out, b) == d
+            assert bt.encoded(enc, b) == O.rans_encode(tab, N, d)
+    # a decode-only graph over a corrupted buffer 0: the error must be reported
+    # on every replay, and the clean buffers still decoded
+    dg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(dg, stream=side):
+        bt.decode(enc, out, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    e0 = bt.enc_off_host[0]
+    enc[e0 + 8 * N: e0 + 8 * N + 4] = torch.tensor([0xFF, 0xFF, 0xFF, 0x7F], dtype=torch.uint8).cuda()
+    for _ in range(2):
+        dg.replay()
+        torch.cuda.synchronize()
+        st = bt.statuses()
+        assert st[0] != 0 and st[1] == 0 and st[2] == 0
+        assert bt.raw_of(out, 1) == ds[1] and bt.raw_of(out, 2) == ds[2]
+
+
+def test_host_staging_calls_refuse_capture():
+    from zipora_amd import _lib
+    bt = RansDeviceBatch([1000], 4, shared_table=True)
+    t = zr.Rans64Encoder([1] * 256, 4).table
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    st = None
+    with torch.cuda.graph(g, stream=side):
+        arr = (_lib.RansTable * 1)(t)
+        st = zr.load().zr_rans_dtab_upload(arr, 1, bt.tables.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert st == _lib.ZR_UNSUPPORTED

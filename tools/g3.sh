@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread > gpurun_out/gputests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 170 --timeout-method thread > gpurun_out/gputests.log 2>&1
 echo "gputests rc=$?"
 tail -3 gpurun_out/gputests.log
 timeout -k 10 400 bash tools/ab_multi.sh "zipora_amd/ab/lib_base.so zipora_amd/ab/lib_new.so" > gpurun_out/ab3.log 2>&1

@@ -177,6 +177,7 @@ SIGNATURES = [
     ("zr_memcpy_h2d", ctypes.c_int32, [c_vp, c_vp, c_sz, c_vp]),
     ("zr_memcpy_d2h", ctypes.c_int32, [c_vp, c_vp, c_sz, c_vp]),
     ("zr_memset_dev", ctypes.c_int32, [c_vp, ctypes.c_int, c_sz, c_vp]),
+    ("zr_release_call_contexts", ctypes.c_int32, []),
     ("zr_memcpy_dev", ctypes.c_int32, [c_vp, c_vp, c_sz, ctypes.c_uint32, c_vp]),
     ("zr_stream_sync", ctypes.c_int32, [c_vp]),
     ("zr_timer_enable", ctypes.c_int32, [ctypes.c_int32]),

@@ -73,8 +73,19 @@ int32_t CallLease::acquire() {
     return ZR_OK;
 }
 
+// buffers larger than this are returned when the lease ends (a rare huge call
+// must not pin GiBs of device memory in an idle pooled context for the life of
+// the process); smaller ones stay cached for the next call
+constexpr size_t LEASE_KEEP = size_t(1) << 30;
+
 CallLease::~CallLease() {
     if (!c_) return;
+    for (int i = 0; i < CallCtx::NBUF; i++)
+        if (c_->buf[i] && c_->cap[i] > LEASE_KEEP) {
+            (void)hipFreeAsync(c_->buf[i], c_->stream);  // after the call's work, in stream order
+            c_->buf[i] = nullptr;
+            c_->cap[i] = 0;
+        }
     (void)hipStreamSynchronize(c_->stream);  // nothing of this call may still run
     std::lock_guard<std::mutex> g(g_ctx_mx);
     g_ctx_free[c_->device].push_back(c_);
@@ -83,24 +94,52 @@ CallLease::~CallLease() {
 int32_t CallLease::get(int slot, size_t bytes, void **p) {
     if (bytes == 0) bytes = 16;
     if (bytes > c_->cap[slot]) {
-        // the stream is idle between calls and every call drains it before
-        // returning, so the old buffer is free; grow to the next power of two
-        // (at least 64 KiB) so that a run of growing calls reallocates rarely
+        // grow to the next power of two (at least 64 KiB) so that a run of
+        // growing calls reallocates rarely. Stream-ordered free and allocation
+        // (hipFreeAsync / hipMallocAsync on the context's own stream): growing
+        // never synchronises the device, only this call's stream orders it
         size_t want = 64 << 10;
         while (want < bytes) want <<= 1;
         if (c_->buf[slot]) {
-            ZR_HIP(hipStreamSynchronize(c_->stream));
-            ZR_HIP(hipFree(c_->buf[slot]));
+            ZR_HIP(hipFreeAsync(c_->buf[slot], c_->stream));
             c_->buf[slot] = nullptr;
             c_->cap[slot] = 0;
         }
-        if (dev_alloc(&c_->buf[slot], want) != hipSuccess) {
+        g_dev_allocs.fetch_add(1, std::memory_order_relaxed);
+        if (hipMallocAsync(&c_->buf[slot], want, c_->stream) != hipSuccess) {
             c_->buf[slot] = nullptr;
-            return set_error(ZR_MEMORY_ERROR, "hipMalloc failed");
+            return set_error(ZR_MEMORY_ERROR, "hipMallocAsync failed");
         }
         c_->cap[slot] = want;
     }
     *p = c_->buf[slot];
+    return ZR_OK;
+}
+
+// every idle pooled context of every device: buffers freed, streams destroyed,
+// the devices' default memory pools trimmed (contexts in use are not in the
+// pool and are left alone)
+int32_t release_call_contexts() {
+    std::map<int, std::vector<CallCtx *>> take;
+    {
+        std::lock_guard<std::mutex> g(g_ctx_mx);
+        take.swap(g_ctx_free);
+    }
+    int cur = 0;
+    ZR_HIP(hipGetDevice(&cur));
+    for (auto &kv : take) {
+        ZR_HIP(hipSetDevice(kv.first));
+        for (CallCtx *c : kv.second) {
+            for (int i = 0; i < CallCtx::NBUF; i++)
+                if (c->buf[i]) (void)hipFreeAsync(c->buf[i], c->stream);
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamDestroy(c->stream);
+            delete c;
+        }
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, kv.first) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
+    }
+    ZR_HIP(hipSetDevice(cur));
     return ZR_OK;
 }
 
@@ -288,7 +327,10 @@ int32_t zr_rans_dtab_upload(const zr_rans_table *tables, uint32_t n_tables, void
     clear_error();
     if (n_tables == 0) return ZR_OK;
     // the tables leave from a heap copy that a stream-ordered host callback
-    // frees after the copy (no host synchronisation)
+    // frees after the copy (no host synchronisation); a captured graph would
+    // replay the copy from freed memory, so capture is refused
+    if (capturing((hipStream_t)stream))
+        return set_error(ZR_UNSUPPORTED, "zr_rans_dtab_upload stages host tables: not capturable");
     auto *h = new std::vector<RansDTab>(n_tables);
     for (uint32_t i = 0; i < n_tables; i++) rans_dtab_from_table(&tables[i], &(*h)[i]);
     hipStream_t s = (hipStream_t)stream;
@@ -448,6 +490,12 @@ int32_t zr_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
     ZR_GUARD_BEGIN
     ZR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
     return ZR_OK;
+    ZR_GUARD_END
+}
+int32_t zr_release_call_contexts(void) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    return release_call_contexts();
     ZR_GUARD_END
 }
 int32_t zr_memset_dev(void *dst, int value, size_t bytes, void *stream) {

@@ -804,6 +804,8 @@ int32_t zr_huff_decode_dev(const zr_huff_tree *t, const uint8_t *in, size_t in_l
         return ZR_OK;
     }
     if (ws_bytes < zr_huff_workspace_bytes(0, in_len)) return set_error(ZR_INVALID_INPUT, "workspace too small");
+    if (capturing(s))  // the decode table is staged from host memory freed by a host callback
+        return set_error(ZR_UNSUPPORTED, "zr_huff_decode_dev stages its decode table: not capturable");
     std::vector<uint32_t> lut;
     huff_lut(t, lut);
     if (lut.size() > 256 * 256) return set_error(ZR_INTERNAL, "decode table too large");

@@ -15,6 +15,11 @@ namespace zr {
 int32_t set_error(int32_t code, const std::string &msg);
 // compute units of the current device (cached per device)
 uint32_t cu_count();
+// the stream is being captured into a HIP graph
+inline bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
 void clear_error();
 
 #define ZR_HIP(expr)                                                                       \

@@ -2793,7 +2793,10 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
     const uint64_t gx = (uint64_t)w.nblk * a.B;
     uint64_t epoch = 0;
     if (bt->max_len >= a.N && a.N > 1) {
-        if (w.nblk > SCAN_FUSE) {  // the block sums and their scan first
+        // the fused header read needs a per-call epoch from a host counter: a
+        // graph replay would repeat it, so a capturing stream takes the
+        // k_dec_hdr + k_scan path (capture-safe: no host state)
+        if (w.nblk > SCAN_FUSE || capturing(s)) {  // the block sums and their scan first
             hipLaunchKernelGGL(k_dec_hdr, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
             hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 1);
         } else {  // the decoder reads the lengths itself (see k_dec_xn_fast)
