@@ -97,6 +97,12 @@ int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches);
  * above. freq in 1..4096. Host arrays; synchronous. */
 int32_t zr_rans_symbol_fast_div(uint32_t start, uint32_t freq, const uint64_t *x, size_t n, uint64_t *q,
                                 uint64_t *r);
+/* Diagnostic (no reference counterpart): the number of streams / records the
+ * fast device decoders handed to their generic per-lane loop on the current
+ * device since the last reset (a lane whose reads outran its LDS ring, a state
+ * outside [2^16, 2^24), a table that is not normal). Waits for the device;
+ * reset != 0 zeroes the counter after reading it. */
+int32_t zr_rans_fallback_lanes(uint64_t *count, int32_t reset);
 
 /* ---- device-resident batch pipeline (the GPU hot path) ----
  * A batch is B independent buffers, each coded as one reference rANS stream

@@ -7,8 +7,8 @@ no CPU fallback.
 from ._lib import load, last_error, LIB_PATH  # noqa: F401
 from .errors import ZiporaError  # noqa: F401
 from .rans import (AdaptiveRans64Encoder, ParallelVariant, ParallelX1, ParallelX2, ParallelX4,  # noqa: F401
-                   ParallelX8, Rans64Decoder, Rans64Encoder, Rans64Symbol, device_alloc_count, histogram,
-                   selftest_reciprocal)
+                   ParallelX8, Rans64Decoder, Rans64Encoder, Rans64Symbol, device_alloc_count, fallback_lanes,
+                   histogram, selftest_reciprocal)
 
 __version__ = "0.1.0"
 

@@ -80,6 +80,7 @@ SIGNATURES = [
     ("zr_histogram_allreduce_dev", ctypes.c_int32, [c_vp, c_vp, ctypes.c_uint32, c_vp]),
     ("zr_table_broadcast_dev", ctypes.c_int32, [c_vp, c_vp, ctypes.c_uint32, ctypes.c_int32, c_vp]),
     ("zr_comm_destroy", ctypes.c_int32, [c_vp]),
+    ("zr_rans_fallback_lanes", ctypes.c_int32, [c_u64p, ctypes.c_int32]),
     ("zr_rans_symbol_fast_div", ctypes.c_int32, [ctypes.c_uint32, ctypes.c_uint32, c_u64p, c_sz, c_u64p, c_u64p]),
     ("zr_device_alloc_count", ctypes.c_int32, [c_u64p]),
     ("zr_rans_dtab_bytes", c_sz, []),

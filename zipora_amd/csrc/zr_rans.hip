@@ -1135,6 +1135,11 @@ constexpr int RR = 32;   // ring rows (dwords) per lane
 // One lane decodes stream s generically (decode_symbol, rans.rs:472-507: u64
 // state, byte-wise renormalisation, any table kind): the fast decoder's fallback.
 // Returns false on "Insufficient data for decoding" (rans.rs:480-482).
+// lanes/records the fast decoders handed to their generic per-lane loops
+// (zr_rans_fallback_lanes): a counter for tests and the bench, so that a
+// refill schedule that outruns its ring shows as a number, not only as time
+__device__ unsigned long long g_dec_fallbacks;
+
 __device__ __noinline__ bool dec_lane_generic(const RansDTab *T, const uint32_t *lds_slot, const uint8_t *sb,
                                               uint32_t L, uint64_t X, uint64_t c, uint8_t *obuf, uint32_t N,
                                               uint32_t s) {
@@ -1544,6 +1549,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             row += 2 * N;
         }
     };
+    uint32_t ppos8 = pos8 + TW * 8;  // wide shape: pos8 at the previous boundary (first: one byte a step)
     auto boundary_w = [&](uint32_t t, bool pk) {
         bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if (t >= 1) {
@@ -1554,12 +1560,20 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
                 asm volatile("s_waitcnt vmcnt(8)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
             else
                 asm volatile("s_waitcnt vmcnt(32)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
-            if (pnd) {
+            // the segment lands once every byte of the ring rows it takes is
+            // consumed; otherwise the load below fetches it again
+            if (pnd && (int32_t)(pos8 - lov8()) <= 64 * 8) {
                 land(e0, e1, e2, e3);
                 pnd = false;
             }
         }
-        const bool issue = !(ABL & 4) && active && (int32_t)(pos8 - lov8()) <= 64 * 8;
+        // issue when the lane will have consumed the rows by the next boundary,
+        // predicting that the next tile consumes what the last one did (a one-tile
+        // lag with the 16-step tiles' "<= 64 unread" rule left 0-32 bytes at the
+        // landing and sent most lanes to the generic decoder)
+        const uint32_t used8 = ppos8 - pos8;
+        ppos8 = pos8;
+        const bool issue = !(ABL & 4) && active && (int32_t)(pos8 - used8 - lov8()) <= 64 * 8;
         const uintptr_t g = !issue ? dummy : clampa(lo64 - 64);
         asm_load16(e0, g);
         asm_load16_off<16>(e1, g);
@@ -1601,7 +1615,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         if constexpr (PF) {
             if (pnd_o) land(o0, o1, o2, o3);
             if (pnd_e) land(e0, e1, e2, e3);
-        } else if (pnd) {  // (wide shape: the one staging set)
+        } else if (pnd && (int32_t)(pos8 - lov8()) <= 64 * 8) {  // (wide shape: the one staging set)
             land(e0, e1, e2, e3);
         }
         uint32_t pos_snap = pos8;
@@ -1628,6 +1642,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         }
         if (active) {
             if (bad) {
+                atomicAdd(&g_dec_fallbacks, 1ull);
                 generic();
             } else {
                 // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
@@ -2442,6 +2457,7 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
     if (fast) {
         int32_t st;
         if (bad) {
+            atomicAdd(&g_dec_fallbacks, 1ull);
             st = x1_dec_generic(T, lds, normal, e, len, X, out, n) ? ZR_OK : ZR_INVALID_INPUT;
         } else {
             // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
@@ -2619,6 +2635,22 @@ int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches) {
     ZR_HIP(hipMemcpyAsync(meta, d, 8, hipMemcpyDeviceToHost, s));
     if ((st = L.sync())) return st;
     *mismatches = meta[0];
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_rans_fallback_lanes(uint64_t *count, int32_t reset) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!count) return set_error(ZR_INVALID_INPUT, "null argument");
+    ZR_HIP(hipDeviceSynchronize());
+    unsigned long long v = 0;
+    ZR_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_dec_fallbacks), sizeof(v), 0, hipMemcpyDeviceToHost));
+    *count = v;
+    if (reset) {
+        v = 0;
+        ZR_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dec_fallbacks), &v, sizeof(v), 0, hipMemcpyHostToDevice));
+    }
     return ZR_OK;
     ZR_GUARD_END
 }

@@ -141,6 +141,14 @@ def selftest_reciprocal():
     return v.value
 
 
+def fallback_lanes(reset=True):
+    """Streams/records the fast device decoders sent to their generic per-lane
+    loop since the last reset (diagnostic; waits for the device)."""
+    v = ctypes.c_uint64(0)
+    check(_lib.load().zr_rans_fallback_lanes(ctypes.byref(v), 1 if reset else 0))
+    return v.value
+
+
 def device_alloc_count():
     v = ctypes.c_uint64(0)
     check(_lib.load().zr_device_alloc_count(ctypes.byref(v)))
@@ -155,4 +163,4 @@ def histogram(data):
 
 __all__ = ["ParallelVariant", "ParallelX1", "ParallelX2", "ParallelX4", "ParallelX8",
            "Rans64Encoder", "Rans64Decoder", "Rans64Symbol", "AdaptiveRans64Encoder", "ZiporaError", "histogram",
-           "selftest_reciprocal", "device_alloc_count"]
+           "selftest_reciprocal", "device_alloc_count", "fallback_lanes"]
