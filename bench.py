@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--workload", default="rans", choices=["rans", "fse", "o1", "blob"],
                    help="rans = BASELINE metric (configs[1]); fse = configs[2]; o1 = configs[3] "
                         "(per-GPU shard); blob = configs[4] (per-GPU batch) -- secondary lines")
+    p.add_argument("--groups", type=int, default=1,
+                   help="rans: code the buffers as G groups on G HIP streams after the shared table "
+                        "(encode+compaction+decode of one group overlap the others')")
     p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--fse-block-kib", type=int, default=64)
     return p.parse_args()
@@ -292,7 +295,8 @@ COPY_NOTE = None
 
 def copy_ceiling(torch, dev, L, nbytes=256 << 20, reps=20):
     """Device-to-device copy of 256 MiB by the library's 16-B-per-lane streaming
-    kernel (zr_memcpy_dev, four loads in flight per lane), read + write bytes /
+    kernel (zr_memcpy_dev: each wave its own contiguous chunk, eight 16-B loads
+    per lane in flight, non-temporal), read + write bytes /
     time, the best of three grid sizes, timed with HIP events on the stream it
     runs on: the practical one-pass ceiling reported beside the 8 TB/s spec peak."""
     global COPY_GBS, COPY_NOTE
@@ -318,7 +322,8 @@ def copy_ceiling(torch, dev, L, nbytes=256 << 20, reps=20):
             if gbs > best:
                 best, best_g = gbs, g
         COPY_GBS = best
-        COPY_NOTE = f"zr_memcpy_dev 256 MiB, 16 B/lane, grid {best_g} x 256, read+write bytes / time"
+        COPY_NOTE = (f"zr_memcpy_dev 256 MiB, per-wave chunks, 8 x 16 B/lane in flight, grid {best_g} x 256, "
+                     "read+write bytes / time")
         del a, b
     return COPY_GBS
 
@@ -576,13 +581,37 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     # (zr_comm_*; the unique id travels over the torch process group, host side)
     comm = zd.RcclComm(world, rank) if world > 1 else None
 
+    # --groups G > 1: after the shared table, the B buffers are coded as G groups
+    # of B / G on G streams (each group its own batch and workspace over the same
+    # table), so one group's compaction and decode overlap the others' encoding
+    G = max(1, getattr(args, "groups", 1)) if B % max(1, getattr(args, "groups", 1)) == 0 else 1
+    groups = []
+    if G > 1:
+        bg = B // G
+        for g in range(G):
+            sub = RansDeviceBatch([n] * bg, N, device=dev, shared_table=True)
+            sub.cbatch.tables = bt.tables.data_ptr()  # the whole batch's table
+            lo, hi = g * bg * n, (g + 1) * bg * n
+            eo = bt.enc_off_host[g * bg]
+            groups.append((sub, raw[lo:hi], enc[eo:], out[lo:hi], torch.cuda.Stream(dev)))
+        ev_tab = torch.cuda.Event()
+
     def step():
         bt.histogram(raw, stream, zeroed=consume)
         if comm is not None:  # in-place u32 all-reduce of the 256 counts over xGMI
             comm.allreduce_histogram(bt.hist, stream.cuda_stream)
         bt.tables_from_hist(stream, consume=consume)
-        bt.encode(raw, enc, stream)
-        bt.decode(enc, out, stream)
+        if G == 1:
+            bt.encode(raw, enc, stream)
+            bt.decode(enc, out, stream)
+            return
+        ev_tab.record(stream)
+        for sub, r, e, o, st in groups:
+            st.wait_event(ev_tab)
+            sub.encode(r, e, st)
+            sub.decode(e, o, st)
+        for *_, st in groups:
+            stream.wait_stream(st)
 
     step()
     torch.cuda.synchronize(dev)
@@ -598,7 +627,12 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
         bt.raise_on_error()
         if not torch.equal(out, raw):
             raise SystemExit("decode mismatch in timed region")
-    comp_bytes = int(bt.enc_len.sum().item())
+    if G > 1:  # the groups' statuses and lengths
+        for sub, *_ in groups:
+            sub.raise_on_error()
+        comp_bytes = sum(int(sub.enc_len.sum().item()) for sub, *_ in groups)
+    else:
+        comp_bytes = int(bt.enc_len.sum().item())
     value = world * total * args.steps / dt / 2**30
     if comm is not None:
         comm.close()

@@ -1173,7 +1173,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
 // streams, e.g. one buffer x 4096 streams, over that many CUs).
 // ABL: diagnostic ablations for profiling only, ZR_DIAG builds (1: no output
 // stores, 2: no slot table read, 4: no ring refills, 8: per-workgroup timeline
-// records written to the workspace scratch area); the product instantiates ABL = 0.
+// records written to the workspace scratch area; wide shape only: 64 refills
+// land without their LDS writes, 128 refill loads read a table line instead of
+// the stream, 256 every store of a wave goes to the same 256 B, 512 no wait for
+// the refill loads at the boundaries); the product instantiates ABL = 0.
 //
 // epoch (non-zero): this kernel also does k_dec_hdr's work (nblk <= SCAN_FUSE):
 // every workgroup reads all N stream lengths of its buffer for its own offset
@@ -1339,7 +1342,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     auto clampa = [&](uintptr_t p) -> uintptr_t { return p > lo_lim ? p : lo_lim; };
     uint32_t *lring = ring + tid;
     // write the 64-B segment at absolute address g (64-aligned; cK = bytes g+16K..)
-    auto put_seg = [&](uint32_t g, const v4u c0, const v4u c1, const v4u c2, const v4u c3) {
+    auto put_seg = [&](uint32_t g, const v4u c0, const v4u c1, const v4u c2, const v4u c3) __attribute__((always_inline)) {
         const uint32_t r0 = ((g >> 2) + 1) & (RR - 1);  // 1 or 17
         uint32_t *p = lring + r0 * FW;
         p[0 * FW] = c0.x; p[1 * FW] = c0.y; p[2 * FW] = c0.z; p[3 * FW] = c0.w;
@@ -1375,13 +1378,13 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     uint32_t pos8 = (uint32_t)pend << 3;  // bytes [.., pos) not yet consumed
     uint32_t x = (uint32_t)X;
     // D: the 4 stream bytes below p (byte p-1 on top)
-    auto readD = [&](uint32_t p8) -> uint32_t {
+    auto readD = [&](uint32_t p8) -> uint32_t __attribute__((always_inline)) {
         const uint32_t *q = lring + ((p8 >> 5) & (RR - 1)) * FW;
         return __builtin_amdgcn_alignbit(q[FW], q[0], p8);
     };
     // one decode step (rans.rs:472-507): renormalise from window D, decode, return
     // the slot entry; hi/lo are the shifted (x : D) pair, sft = 8 + 8 * bytes consumed
-    auto step = [&](uint32_t D, uint32_t &hi, uint32_t &lo, uint32_t &sft) -> uint32_t {
+    auto step = [&](uint32_t D, uint32_t &hi, uint32_t &lo, uint32_t &sft) -> uint32_t __attribute__((always_inline)) {
         sft = __builtin_clz(x) & 24;
         const uint64_t t = ((((uint64_t)x) << 32) | D) << sft;
         hi = (uint32_t)(t >> 32);
@@ -1433,14 +1436,14 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     const uint32_t nfull = PF ? (uint32_t)((cmax - 1) / DT2) : (uint32_t)((n / N) / TW);
     auto lov8 = [&]() -> uint32_t { return PF ? lo8 : (uint32_t)lo64 << 3; };
     // a segment lands: the staging set becomes the 64 bytes below the resident ones
-    auto land = [&](const v4u c0, const v4u c1, const v4u c2, const v4u c3) {
+    auto land = [&](const v4u c0, const v4u c1, const v4u c2, const v4u c3) __attribute__((always_inline)) {
         if constexpr (PF) {
             lo8 -= 512;
             lo -= 64;
             put_seg(lo8 >> 3, c0, c1, c2, c3);
         } else {
             lo64 -= 64;
-            put_seg((uint32_t)lo64, c0, c1, c2, c3);
+            if (!(ABL & 64)) put_seg((uint32_t)lo64, c0, c1, c2, c3);
         }
     };
 
@@ -1452,10 +1455,10 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
 
     // tile boundary t, staging set (s0..s3) = the set of parity t & 1, pmine its
     // in-flight flag
-    auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3, bool &pmine, bool pother) {
+    auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3, bool &pmine, bool pother) __attribute__((always_inline)) {
         // every read of the previous tile was at or above pos - 4 (the no-refill
         // ablation reads stale ring bytes on purpose: no fallback there)
-        bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        bad |= !(ABL & (4 | 64 | 128)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if (t >= 2) {
             // wait for the loads of boundary t-2: younger are the 16 stores of tile
             // t-2, the 4 loads of boundary t-1 and the 16 stores of tile t-1 (every
@@ -1485,7 +1488,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         }
     };
     // DT2 steps in pairs; one ring read per pair
-    auto tile = [&](uint32_t t) {
+    auto tile = [&](uint32_t t) __attribute__((always_inline)) {
         uint32_t D = readD(pos8);
         orsrc = byte_rsrc(outb + (uint64_t)t * DT2 * N);
         uint32_t row = 0;
@@ -1516,9 +1519,9 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // 4g..4g+3 of its stream) are transposed by two DPP lane swaps + v_perm,
     // so lane 4q + r stores row 4g + r of streams 4q..4q+3: 8 dword stores per
     // tile instead of 32 byte stores.
-    auto tile_w = [&](uint32_t t, bool pk) {
+    auto tile_w = [&](uint32_t t, bool pk) __attribute__((always_inline)) {
         uint32_t D = readD(pos8);
-        orsrc = byte_rsrc(outb + (uint64_t)t * TW * N);
+        orsrc = byte_rsrc(outb + ((ABL & 256) ? 0 : (uint64_t)t * TW * N));
         uint32_t row = 0, pk0 = 0;
 #pragma unroll
         for (int j = 0; j < (int)TW / 2; j++) {
@@ -1540,7 +1543,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
                     q = __builtin_amdgcn_perm(x, q, psel1);
                     x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0xB1, 0xF, 0xF, false);  // lane ^ 1
                     q = __builtin_amdgcn_perm(x, q, psel2);
-                    __builtin_amdgcn_raw_buffer_store_b32(q, orsrc, voff_pk, row - 2 * N, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(q, orsrc, voff_pk, (ABL & 256) ? 0 : row - 2 * N, 0);
                 }
             } else {
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, voff, row, 0);
@@ -1550,35 +1553,72 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         }
     };
     uint32_t ppos8 = pos8 + TW * 8;  // wide shape: pos8 at the previous boundary (first: one byte a step)
-    auto boundary_w = [&](uint32_t t, bool pk) {
-        bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+#ifndef ZR_DEC_PAIR
+#define ZR_DEC_PAIR 1
+#endif
+    // PAIR: a refill that starts a 128-B line (the segment below lo64 is the
+    // line's upper half) loads the lower half too, into the second staging set
+    // (o), which lands from registers at a later boundary: both halves of every
+    // line are requested together, instead of the lower half 64 steps later,
+    // when the L2 has usually evicted the line (the decoder's FETCH_SIZE was
+    // 1.83x its stream bytes)
+    constexpr bool PAIR = ZR_DEC_PAIR && !PF;
+    bool hasB = false;  // PAIR: o holds the segment below e's, loaded, not yet landed
+    auto boundary_w = [&](uint32_t t, bool pk) __attribute__((always_inline)) {
+        bad |= !(ABL & (4 | 64 | 128)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if (t >= 1) {
             // the loads of boundary t - 1; younger: tile t-1's stores
-            if (ABL & 1)
-                asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
+            if (ABL & 512)
+                asm volatile("" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1), "+v"(o2),
+                             "+v"(o3)::"memory");
+            else if (ABL & 1)
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
+                             "+v"(o2), "+v"(o3)::"memory");
             else if (pk)
-                asm volatile("s_waitcnt vmcnt(8)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
+                asm volatile("s_waitcnt vmcnt(8)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
+                             "+v"(o2), "+v"(o3)::"memory");
             else
-                asm volatile("s_waitcnt vmcnt(32)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
+                asm volatile("s_waitcnt vmcnt(32)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
+                             "+v"(o2), "+v"(o3)::"memory");
             // the segment lands once every byte of the ring rows it takes is
             // consumed; otherwise the load below fetches it again
-            if (pnd && (int32_t)(pos8 - lov8()) <= 64 * 8) {
-                land(e0, e1, e2, e3);
-                pnd = false;
-            }
+            // (flags updated outside the branches: stores to either of two
+            // flags in two branches were merged into one store through a
+            // selected address, which put both flags in scratch memory)
+            const bool landable = (int32_t)(pos8 - lov8()) <= 64 * 8;
+            const bool lE = pnd && landable, lO = PAIR && !pnd && hasB && landable;
+            if (lE) land(e0, e1, e2, e3);
+            if (lO) land(o0, o1, o2, o3);
+            pnd = pnd && !lE;
+            hasB = hasB && !lO;
         }
         // issue when the lane will have consumed the rows by the next boundary,
         // predicting that the next tile consumes what the last one did (a one-tile
         // lag with the 16-step tiles' "<= 64 unread" rule left 0-32 bytes at the
-        // landing and sent most lanes to the generic decoder)
+        // landing and sent most lanes to the generic decoder). A lane whose o
+        // still holds the next segment issues nothing new. A segment that did not
+        // land is fetched again whether or not the prediction still asks for it:
+        // dropping it while o holds the one below would land o in its place.
         const uint32_t used8 = ppos8 - pos8;
         ppos8 = pos8;
-        const bool issue = !(ABL & 4) && active && (int32_t)(pos8 - used8 - lov8()) <= 64 * 8;
-        const uintptr_t g = !issue ? dummy : clampa(lo64 - 64);
+        const bool need = !(ABL & 4) && active && (int32_t)(pos8 - used8 - lov8()) <= 64 * 8;
+        const bool issue = pnd || (need && !hasB);
+        const uintptr_t g = (!issue || (ABL & 128)) ? dummy : clampa(lo64 - 64);
         asm_load16(e0, g);
         asm_load16_off<16>(e1, g);
         asm_load16_off<32>(e2, g);
         asm_load16_off<48>(e3, g);
+        if constexpr (PAIR) {
+            const bool pair = issue && !pnd && !hasB && (lo64 & 127) == 0 && lo64 - 128 >= lo_lim && !(ABL & 128);
+            if (pair) {  // (tied operands: the phi at the merge keeps o in place)
+                const uintptr_t gb = lo64 - 128;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(o0) : "v"(gb) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "+v"(o1) : "v"(gb) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "+v"(o2) : "v"(gb) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:48" : "+v"(o3) : "v"(gb) : "memory");
+            }
+            hasB = hasB || pair;
+        }
         pnd = issue;
     };
     if (!PF && wave_live) {
@@ -1611,12 +1651,14 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         // ---- last tile (1..DT2 steps): every segment in flight lands first
         asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
                      "+v"(o2), "+v"(o3)::"memory");
-        bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        bad |= !(ABL & (4 | 64 | 128)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if constexpr (PF) {
             if (pnd_o) land(o0, o1, o2, o3);
             if (pnd_e) land(e0, e1, e2, e3);
-        } else if (pnd && (int32_t)(pos8 - lov8()) <= 64 * 8) {  // (wide shape: the one staging set)
-            land(e0, e1, e2, e3);
+        } else {  // (wide shape: e, then PAIR's o)
+            const bool lE = pnd && (int32_t)(pos8 - lov8()) <= 64 * 8;
+            if (lE) land(e0, e1, e2, e3);
+            if (PAIR && !(pnd && !lE) && hasB && (int32_t)(pos8 - lov8()) <= 64 * 8) land(o0, o1, o2, o3);
         }
         uint32_t pos_snap = pos8;
         const uint64_t k0 = (uint64_t)nfull * (PF ? DT2 : TW);
@@ -1625,7 +1667,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         for (uint32_t j = 0; j < nst; j++) {
             const uint64_t k = k0 + j;
             const bool live = k < c;
-            if (live) bad |= !(ABL & 4) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+            if (live) bad |= !(ABL & (4 | 64 | 128)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
             uint32_t h, l, sf;
             const uint32_t ent = step(readD(pos8), h, l, sf);
             pos8 = pos8 + 8 - sf;
@@ -2859,6 +2901,12 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
                 case 32: kern = k_dec_xn_fast<1024, 32>; break;
                 case 21: kern = k_dec_xn_fast<1024, 21>; break;
                 case 37: kern = k_dec_xn_fast<1024, 37>; break;
+                case 64: kern = k_dec_xn_fast<1024, 64>; break;
+                case 128: kern = k_dec_xn_fast<1024, 128>; break;
+                case 192: kern = k_dec_xn_fast<1024, 192>; break;
+                case 256: kern = k_dec_xn_fast<1024, 256>; break;
+                case 512: kern = k_dec_xn_fast<1024, 512>; break;
+                case 576: kern = k_dec_xn_fast<1024, 576>; break;
                 default: break;
             }
 #else
