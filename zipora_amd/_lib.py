@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(_PKG, "libzipora_amd.so")
 # read ZR_ABLATE / ZR_DEC_ABL / ZR_COMPACT_OLD), ZR_LIB_PATH another build (A/B
 # runs); bench.py refuses to print a metric line under either
 DIAG_LIB_PATH = os.path.join(_PKG, "libzipora_amd_diag.so")
-DIAG_ENV = ("ZR_DIAG_LIB", "ZR_LIB_PATH", "ZR_ABLATE", "ZR_DEC_ABL", "ZR_COMPACT_OLD")
+DIAG_ENV = ("ZR_CMP_ABL", "ZR_DIAG_LIB", "ZR_LIB_PATH", "ZR_ABLATE", "ZR_DEC_ABL", "ZR_COMPACT_OLD")
 
 
 def diag_env():

@@ -87,6 +87,7 @@ void rans_dtab_from_table(const zr_rans_table *t, RansDTab *d);
 struct RansWork {
     uint32_t *st_state;   // [B*N]
     uint32_t *st_len;     // [B*N]
+    uint32_t *st_off;     // [B*N] (256-lane encoder) byte offset of each stream in its 256-stream block
     uint64_t *blocksum;   // [B*nblk]
     uint64_t *blockoff;   // [B*nblk]
     uint8_t *scratch;     // [B*R]

@@ -674,7 +674,12 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         // one reduction (no extra LDS: the workgroup's 40 KiB are exact for four
         // per CU): bytes (< 2^40) and, from bit 55, the count of lanes in error
         unsigned long long *sh = reinterpret_cast<unsigned long long *>(itile);
-        const uint64_t r = block_sum((active ? bytes : 0) | ((uint64_t)bad << 55), sh);
+        uint64_t r;
+        const uint64_t ex = block_excl_scan((active ? bytes : 0) | ((uint64_t)bad << 55), sh, &r);
+        // the stream's offset in the block: the compaction reads its 16 streams'
+        // offsets instead of scanning the block again (a block's bytes < 2^32:
+        // the compaction uses this only for buffers below 4 GiB)
+        if (active) w.st_off[(size_t)b * N + s] = (uint32_t)(ex & ((1ull << 55) - 1));
         if (tid == 0) w.blocksum[(size_t)b * w.nblk + blk] = (r & ((1ull << 55) - 1)) | ((r >> 55) ? BS_ERR : 0);
     } else {  // narrow workgroups add their wave sums into the zeroed block sum
         const uint64_t ws = wave_sum(active ? bytes : 0);
@@ -789,9 +794,11 @@ __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, Ra
 // chunks quad-major (lane = stream of the group), so each load instruction
 // reads the group's quad q as one 256-B run; chunks outside a stream's range
 // in the window are skipped lanes.
-template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL>  // streams per group (divides 64), window bytes, loads in flight
+// ABL (ZR_DIAG builds, profiling only): 1 no phase-2 global stores, 2 no phase-1
+// LDS image writes, 4 phase-1 loads all read the group's first 256 B
+template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0>  // streams per group (divides 64), window bytes, loads in flight
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_lds(
-    uint8_t *enc, KArgs a, RansWork w, uint32_t nwin) {
+    uint8_t *enc, KArgs a, RansWork w, uint32_t nwin, int has_off) {
     static_assert(CS <= 64 && 64 % CS == 0, "a group's streams are lanes of one wave");
     const uint32_t nblk = w.nblk;
     const uint32_t gpb = 256 / CS;  // groups per 256-stream block
@@ -811,38 +818,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     __shared__ uint32_t slen[CS], cpre[CS + 1], clo[CS], crng[2];
     __shared__ int4 ilm[CS];  // IL, per stream in the window: quad rows [x, y), image bytes [z, w) (z: its quad 0)
     __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
-    // the buffer's scan of block byte sums (k_scan, fused): this block's
-    // offset, and for group 0 the encoded length and the final status
-    // (more than SCAN_FUSE blocks: k_scan ran first and wrote the offsets, the
-    // encoded length and the status)
-    uint64_t bo;
-    bool failed;
-    if (nblk <= SCAN_FUSE) {
-        uint64_t below = 0, all = 0, flagged = 0;
-        for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
-            const uint64_t v = w.blocksum[(size_t)b * nblk + i];
-            const uint64_t c = v & ~BS_ERR;
-            below += i < blk ? c : 0;
-            all += c;
-            flagged |= v >> 63;
-        }
-        // one reduction: the bytes below this block (< 2^55), and above them the
-        // number of threads that saw a block flagged by k_enc_xn
-        const uint64_t r = block_sum(below | (flagged << 55), sh);
-        bo = r & ((1ull << 55) - 1);
-        failed = (r >> 55) != 0;
-        if (grp == 0 && wi == 0) {  // workgroup-uniform: the buffer's status and length
-            const uint64_t tot = block_sum(all, sh);
-            if (threadIdx.x == 0) {
-                a.enc_len[b] = (uint64_t)N * 12 + tot;
-                a.status[b] = failed ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an xN encode
-            }
-        }
-    } else {
-        bo = w.blockoff[(size_t)b * nblk + blk];
-        failed = a.status[b] != 0;
-    }
-    if (failed) return;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wv = tid >> 6;
     uint8_t *dbase = enc + a.enc_off[b] + 12 * (size_t)N;
@@ -896,20 +871,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             }
         }
     };
-    uint64_t span = 0;
-    uintptr_t ua0 = 0;
-    {
-        // offsets of the block's streams (block scan), keep this group's; the
-        // group's first window workgroup writes their states and lengths. The
-        // group's streams are lanes [l0, l0 + ns) of one wave: the group's
-        // extent comes from its first and last lane, and the chunk ranges of
-        // the workgroup's first window are prefixed right here
-        const uint32_t sb = blk * 256 + tid;
-        const uint32_t i = sb - s0;
-        const bool mine = sb >= s0 && i < ns;
-        const uint32_t L = sb < N ? w.st_len[(size_t)b * N + sb] : 0;
-        const uint64_t off = block_excl_scan(L, sh, nullptr) + bo;
-        const uint32_t l0 = (s0 - blk * 256) & 63;
+    // the group's streams: offsets, lengths, header words, first window's chunk
+    // ranges (lanes [l0, l0 + ns) of the calling wave hold streams s0 ..)
+    auto group_setup = [&](bool mine, uint32_t i, uint32_t sb, uint64_t off, uint32_t L, uint32_t l0) {
         const uint64_t g_r0 = __shfl(off, (int)l0, 64);
         const uint64_t g_r1 = __shfl(off + L, (int)(l0 + ns - 1), 64);
         const uintptr_t g_ua0 = ((uintptr_t)dbase + g_r0) & ~(uintptr_t)15;
@@ -934,9 +898,87 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         const uint64_t win0 = (uint64_t)wi * CWIN;
         if (mine && g_r1 > g_r0) chunk_range(off, L, g_ua0, win0, min(g_span, win0 + (uint64_t)CWIN), c0, cnt);
         const int32_t dbias = (int32_t)((int64_t)((uintptr_t)dbase + off - g_ua0) - (int64_t)win0);
-        if (wv == (s0 - blk * 256) / 64) publish(mine, i, c0, cnt, dbias, L, l0);  // the group's wave (uniform branch)
+        publish(mine, i, c0, cnt, dbias, L, l0);
+    };
+    if (has_off && nblk <= SCAN_FUSE) {
+        // the encoder left every stream's offset in its block (st_off): wave 0
+        // alone sums the <= 64 block sums below this block and sets the group
+        // up, one barrier, no block scan
+        __shared__ uint32_t sfail;
+        if (wv == 0) {
+            const uint64_t v = lane < nblk ? w.blocksum[(size_t)b * nblk + lane] : 0;
+            const uint64_t c = v & ~BS_ERR;
+            const uint64_t below = wave_sum(lane < blk ? c : 0);
+            const bool flagged = __any((v >> 63) != 0);
+            if (grp == 0 && wi == 0) {
+                const uint64_t tot = wave_sum(c);
+                if (lane == 0) {
+                    a.enc_len[b] = (uint64_t)N * 12 + tot;
+                    a.status[b] = flagged ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an xN encode
+                }
+            }
+            if (!flagged) {
+                const bool mine = lane < ns;
+                const uint32_t sb = s0 + lane;
+                const uint32_t L = mine ? w.st_len[(size_t)b * N + sb] : 0;
+                const uint64_t off = mine ? (uint64_t)w.st_off[(size_t)b * N + sb] + below : 0;
+                group_setup(mine, lane, sb, off, L, 0);
+            }
+            if (lane == 0) sfail = flagged;
+        }
+        __syncthreads();
+        if (sfail) return;
+    } else {
+    // the buffer's scan of block byte sums (k_scan, fused): this block's
+    // offset, and for group 0 the encoded length and the final status
+    // (more than SCAN_FUSE blocks: k_scan ran first and wrote the offsets, the
+    // encoded length and the status)
+    uint64_t bo;
+    bool failed;
+    if (nblk <= SCAN_FUSE) {
+        uint64_t below = 0, all = 0, flagged = 0;
+        for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
+            const uint64_t v = w.blocksum[(size_t)b * nblk + i];
+            const uint64_t c = v & ~BS_ERR;
+            below += i < blk ? c : 0;
+            all += c;
+            flagged |= v >> 63;
+        }
+        // one reduction: the bytes below this block (< 2^55), and above them the
+        // number of threads that saw a block flagged by k_enc_xn
+        const uint64_t r = block_sum(below | (flagged << 55), sh);
+        bo = r & ((1ull << 55) - 1);
+        failed = (r >> 55) != 0;
+        if (grp == 0 && wi == 0) {  // workgroup-uniform: the buffer's status and length
+            const uint64_t tot = block_sum(all, sh);
+            if (threadIdx.x == 0) {
+                a.enc_len[b] = (uint64_t)N * 12 + tot;
+                a.status[b] = failed ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an xN encode
+            }
+        }
+    } else {
+        bo = w.blockoff[(size_t)b * nblk + blk];
+        failed = a.status[b] != 0;
+    }
+    if (failed) return;
+    {
+        // offsets of the block's streams (block scan), keep this group's; the
+        // group's first window workgroup writes their states and lengths. The
+        // group's streams are lanes [l0, l0 + ns) of one wave: the group's
+        // extent comes from its first and last lane, and the chunk ranges of
+        // the workgroup's first window are prefixed right here
+        const uint32_t sb = blk * 256 + tid;
+        const uint32_t i = sb - s0;
+        const bool mine = sb >= s0 && i < ns;
+        const uint32_t L = sb < N ? w.st_len[(size_t)b * N + sb] : 0;
+        const uint64_t off = block_excl_scan(L, sh, nullptr) + bo;
+        const uint32_t l0 = (s0 - blk * 256) & 63;
+        if (wv == (s0 - blk * 256) / 64) group_setup(mine, i, sb, off, L, l0);  // the group's wave (uniform branch)
     }
     __syncthreads();
+    }
+    uint64_t span = 0;
+    uintptr_t ua0 = 0;
     const uint64_t r0 = soff[0], r1 = soff[ns - 1] + slen[ns - 1];
     if (r1 <= r0) return;
     ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
@@ -1000,10 +1042,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                     nv[k] = min(16u, slen[si] - 16 * c);
                     dpos[k] = (int32_t)((int64_t)((uintptr_t)dbase + soff[si] - ua0) - (int64_t)win) + 16 * (int32_t)c;
                 }
-                v[k] = *reinterpret_cast<const v4u *>(nv[k] ? src : sbase);
+                v[k] = *reinterpret_cast<const v4u *>((nv[k] && !(ABL & 4)) ? src : sbase + (lane % CS) * 16);
             }
             for (uint32_t k = 0; k < CU_LD; k++) {
                 if (!nv[k]) continue;
+                if (ABL & 2) {
+                    asm volatile("" ::"v"(v[k].x), "v"(v[k].w));
+                    continue;
+                }
                 const int32_t p = dpos[k];
                 if (IL && nv[k] == 16 && p >= 0 && p + 16 <= (int32_t)wl) {
                     // the lanes of a row are 16 streams of different alignments
@@ -1065,7 +1111,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             // counts in lgkmcnt, so the LDS waits and barriers after it would
             // wait for the store itself)
             uint8_t *dst = dbase + (int64_t)(ua0 + q0 - (uintptr_t)dbase);
-            if (q0 >= lo && q0 + 16 <= span) {
+            if (ABL & 1) {
+                asm volatile("" ::"v"(*reinterpret_cast<const uint32_t *>(img + 16 * u)));
+            } else if (q0 >= lo && q0 + 16 <= span) {
                 // non-temporal: the encoded streams do not linger dirty in the XCD L2s
                 // (same-box A/B: the decode that reads them 0.200 -> 0.180 ms, the
                 // compaction itself unchanged)
@@ -2589,7 +2637,7 @@ size_t rans_workspace_bytes(uint32_t B, uint32_t N, uint64_t max_len) {
     const uint64_t nblk = ceil_div(N, 256);
     const ScratchGeom g = scratch_geom(N, max_len);
     size_t t = 0;
-    t += round_up((uint64_t)B * N * 4, 256) * 2;
+    t += round_up((uint64_t)B * N * 4, 256) * 3;
     t += round_up((uint64_t)B * nblk * 8, 256) * 2;
     t += (size_t)B * g.region;
     return t + 256;
@@ -2613,6 +2661,7 @@ int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t by
     };
     w->st_state = reinterpret_cast<uint32_t *>(take((uint64_t)B * N * 4));
     w->st_len = reinterpret_cast<uint32_t *>(take((uint64_t)B * N * 4));
+    w->st_off = reinterpret_cast<uint32_t *>(take((uint64_t)B * N * 4));
     w->blocksum = reinterpret_cast<uint64_t *>(take((uint64_t)B * nblk * 8));
     w->blockoff = reinterpret_cast<uint64_t *>(take((uint64_t)B * nblk * 8));
     w->scratch = take((uint64_t)B * w->region);
@@ -2822,8 +2871,27 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             constexpr uint32_t CWIN = 19 * 1024;
             const uint64_t max_span = 16ull * w.cap + 16;
             const uint32_t nwin = (uint32_t)std::max<uint64_t>(1, max_span / CWIN / 2);
-            launch_timed("rans_compact", w.il ? k_enc_compact_lds<16, CWIN, 4, true> : k_enc_compact_lds<16, CWIN, 4, false>,
-                         dim3((uint32_t)(gx * 16 * nwin)), dim3(256), 0, s, enc, a, w, nwin);
+#ifdef ZR_DIAG
+            static const int cabl = getenv("ZR_CMP_ABL") ? atoi(getenv("ZR_CMP_ABL")) : 0;  // profiling only
+            auto kcmp = w.il ? k_enc_compact_lds<16, CWIN, 4, true> : k_enc_compact_lds<16, CWIN, 4, false>;
+            if (w.il) {
+                switch (cabl) {
+                    case 1: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 1>; break;
+                    case 2: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 2>; break;
+                    case 3: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 3>; break;
+                    case 4: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 4>; break;
+                    case 7: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 7>; break;
+                    default: break;
+                }
+            }
+#else
+            auto kcmp = w.il ? k_enc_compact_lds<16, CWIN, 4, true> : k_enc_compact_lds<16, CWIN, 4, false>;
+#endif
+            // the 256-lane encoder leaves each stream's offset in its block (a
+            // block's bytes fit 32 bits: 256 * cap < 2^32)
+            const int has_off = !narrow && 256ull * w.cap < (1ull << 32);
+            launch_timed("rans_compact", kcmp, dim3((uint32_t)(gx * 16 * nwin)), dim3(256), 0, s, enc, a, w, nwin,
+                         has_off);
         }
     }
     timer_begin("rans_encode_x1", s);
