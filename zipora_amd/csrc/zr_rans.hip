@@ -1179,6 +1179,9 @@ __global__ __launch_bounds__(256) void k_dec_hdr(const uint8_t *enc, KArgs a, Ra
 //     store per wave, row offset in an SGPR, no VALU address work.
 // ----------------------------------------------------------------------
 constexpr int RR = 32;   // ring rows (dwords) per lane
+#ifndef ZR_DEC_T8
+#define ZR_DEC_T8 1  // the 1024-lane decoder reads 8-byte slot entries (f | sym << 24, slot - start)
+#endif
 
 // One lane decodes stream s generically (decode_symbol, rans.rs:472-507: u64
 // state, byte-wise renormalisation, any table kind): the fast decoder's fallback.
@@ -1252,7 +1255,14 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // 8-byte entries instead, {f | sym << 24, slot - start}, so the update is one
     // mad_u24 straight on the entry
     constexpr uint32_t TABW = (WT ? 2 : 1) * TOTFREQ;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[TABW + (RR + 1) * FW];
+    // MIR: the ring has a mirror of row 0 at row 32, so a window read is one
+    // ds_read2st64. The wide shape with 8-byte entries has no room for it
+    // (32 KiB table + 32 rows x 1024 lanes = the 160 KiB of the CU): its window
+    // read takes rows r and (r + 1) & 31 separately. SH: the step returns the
+    // slot entry with the symbol in its top byte (wide shape, 8-byte entries)
+    constexpr bool MIR = !(WT && FW == 1024);
+    constexpr bool SH = WT && FW == 1024;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[TABW + (RR + (MIR ? 1 : 0)) * FW];
     uint32_t *ring = lds + TABW;
     // scan scratch and flag alias the ring (used before it is filled)
     unsigned long long *sh = reinterpret_cast<unsigned long long *>(ring);
@@ -1397,7 +1407,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         p[4 * FW] = c1.x; p[5 * FW] = c1.y; p[6 * FW] = c1.z; p[7 * FW] = c1.w;
         p[8 * FW] = c2.x; p[9 * FW] = c2.y; p[10 * FW] = c2.z; p[11 * FW] = c2.w;
         p[12 * FW] = c3.x; p[13 * FW] = c3.y; p[14 * FW] = c3.z;
-        p[15 * FW] = c3.w;                      // row 16, or the mirror row 32
+        if (MIR) p[15 * FW] = c3.w;             // row 16, or the mirror row 32
         lring[((r0 + 15) & (RR - 1)) * FW] = c3.w;  // row 0 itself (r0 = 17; r0 = 1: row 16 again)
     };
     // prologue: the 64-B segment holding the last stream byte and the one below
@@ -1427,7 +1437,14 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     uint32_t x = (uint32_t)X;
     // D: the 4 stream bytes below p (byte p-1 on top)
     auto readD = [&](uint32_t p8) -> uint32_t __attribute__((always_inline)) {
-        const uint32_t *q = lring + ((p8 >> 5) & (RR - 1)) * FW;
+        const uint32_t r = (p8 >> 5) & (RR - 1);
+        if constexpr (!MIR) {  // rows r and r + 1 (mod 32): byte offsets in the ring, the lane's column added
+            const uint32_t o0 = (p8 << 7) & ((RR - 1) * FW * 4), o1 = (o0 + FW * 4) & ((RR - 1) * FW * 4);
+            const char *base = reinterpret_cast<const char *>(ring) + tid * 4;
+            return __builtin_amdgcn_alignbit(*reinterpret_cast<const uint32_t *>(base + o1),
+                                             *reinterpret_cast<const uint32_t *>(base + o0), p8);
+        }
+        const uint32_t *q = lring + r * FW;
         return __builtin_amdgcn_alignbit(q[FW], q[0], p8);
     };
     // one decode step (rans.rs:472-507): renormalise from window D, decode, return
@@ -1440,7 +1457,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         if (WT && !(ABL & 2)) {  // 8-byte entry: x = f * (x >> 12) + (slot - start), sym in the top byte
             const v2u e2 = *reinterpret_cast<const v2u *>(reinterpret_cast<const char *>(lds) + ((hi >> 5) & 0x7FF8));
             x = __umul24(e2.x, hi >> 20) + e2.y;
-            return e2.x >> 24;
+            return SH ? e2.x : e2.x >> 24;
         }
         const uint32_t ent = (ABL & 2) ? (hi & 0x0FFFFF00u) | 0x01000000u
                                        : *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) +
@@ -1583,10 +1600,11 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             if (ABL & 1) {
                 sink += eA ^ eB;
             } else if (pk) {
+                // (SH: the symbols are the entries' top bytes)
                 if ((j & 1) == 0) {
-                    pk0 = __builtin_amdgcn_perm(eB, eA, 0x0c0c0400u);  // [eA, eB, 0, 0]
+                    pk0 = __builtin_amdgcn_perm(eB, eA, SH ? 0x0c0c0703u : 0x0c0c0400u);  // [eA, eB, 0, 0]
                 } else {
-                    uint32_t q = __builtin_amdgcn_perm(eB, eA, 0x04000c0cu) | pk0;  // rows 4g..4g+3
+                    uint32_t q = __builtin_amdgcn_perm(eB, eA, SH ? 0x07030c0cu : 0x04000c0cu) | pk0;  // rows 4g..4g+3
                     uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0x4E, 0xF, 0xF, false);  // lane ^ 2
                     q = __builtin_amdgcn_perm(x, q, psel1);
                     x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0xB1, 0xF, 0xF, false);  // lane ^ 1
@@ -1594,8 +1612,8 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
                     __builtin_amdgcn_raw_buffer_store_b32(q, orsrc, voff_pk, (ABL & 256) ? 0 : row - 2 * N, 0);
                 }
             } else {
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, voff, row, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eB, orsrc, voff, row + N, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? eA >> 24 : eA), orsrc, voff, row, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? eB >> 24 : eB), orsrc, voff, row + N, 0);
             }
             row += 2 * N;
         }
@@ -1671,7 +1689,10 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     };
     if (!PF && wave_live) {
         // packed stores: every lane of the wave a stream, 4-aligned rows
-        const bool pk = __builtin_amdgcn_readfirstlane(
+#ifndef ZR_DEC_PK
+#define ZR_DEC_PK 1
+#endif
+        const bool pk = ZR_DEC_PK && __builtin_amdgcn_readfirstlane(
                             (uint32_t)(wave_all && (N & 3) == 0 && ((((uintptr_t)outb) & 3) == 0))) != 0;
         if (pk) {
             for (uint32_t t = 0; t < nfull; t++) {
@@ -1719,7 +1740,8 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             uint32_t h, l, sf;
             const uint32_t ent = step(readD(pos8), h, l, sf);
             pos8 = pos8 + 8 - sf;
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ent, orsrc, live ? voff : 0x80000000u, (uint32_t)(j * N), 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? ent >> 24 : ent), orsrc, live ? voff : 0x80000000u,
+                                                 (uint32_t)(j * N), 0);
             if (live) pos_snap = pos8;
         }
         if ((ABL & 1) && sink == 0x9E3779B9u) a.status[b] = 7;  // keeps the ablated work live
@@ -2957,28 +2979,28 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
             const uint32_t nblkF = (uint32_t)ceil_div(a.N, 1024);
 #ifdef ZR_DIAG
             static const int abl = getenv("ZR_DEC_ABL") ? atoi(getenv("ZR_DEC_ABL")) : 0;  // profiling only
-            auto kern = k_dec_xn_fast<1024, 0>;
+            auto kern = k_dec_xn_fast<1024, 0, ZR_DEC_T8 != 0>;
             switch (abl) {
-                case 1: kern = k_dec_xn_fast<1024, 1>; break;
-                case 2: kern = k_dec_xn_fast<1024, 2>; break;
-                case 4: kern = k_dec_xn_fast<1024, 4>; break;
-                case 7: kern = k_dec_xn_fast<1024, 7>; break;
-                case 8: kern = k_dec_xn_fast<1024, 8>; break;
-                case 5: kern = k_dec_xn_fast<1024, 5>; break;
-                case 16: kern = k_dec_xn_fast<1024, 16>; break;
-                case 32: kern = k_dec_xn_fast<1024, 32>; break;
-                case 21: kern = k_dec_xn_fast<1024, 21>; break;
-                case 37: kern = k_dec_xn_fast<1024, 37>; break;
-                case 64: kern = k_dec_xn_fast<1024, 64>; break;
-                case 128: kern = k_dec_xn_fast<1024, 128>; break;
-                case 192: kern = k_dec_xn_fast<1024, 192>; break;
-                case 256: kern = k_dec_xn_fast<1024, 256>; break;
-                case 512: kern = k_dec_xn_fast<1024, 512>; break;
-                case 576: kern = k_dec_xn_fast<1024, 576>; break;
+                case 1: kern = k_dec_xn_fast<1024, 1, ZR_DEC_T8 != 0>; break;
+                case 2: kern = k_dec_xn_fast<1024, 2, ZR_DEC_T8 != 0>; break;
+                case 4: kern = k_dec_xn_fast<1024, 4, ZR_DEC_T8 != 0>; break;
+                case 7: kern = k_dec_xn_fast<1024, 7, ZR_DEC_T8 != 0>; break;
+                case 8: kern = k_dec_xn_fast<1024, 8, ZR_DEC_T8 != 0>; break;
+                case 5: kern = k_dec_xn_fast<1024, 5, ZR_DEC_T8 != 0>; break;
+                case 16: kern = k_dec_xn_fast<1024, 16, ZR_DEC_T8 != 0>; break;
+                case 32: kern = k_dec_xn_fast<1024, 32, ZR_DEC_T8 != 0>; break;
+                case 21: kern = k_dec_xn_fast<1024, 21, ZR_DEC_T8 != 0>; break;
+                case 37: kern = k_dec_xn_fast<1024, 37, ZR_DEC_T8 != 0>; break;
+                case 64: kern = k_dec_xn_fast<1024, 64, ZR_DEC_T8 != 0>; break;
+                case 128: kern = k_dec_xn_fast<1024, 128, ZR_DEC_T8 != 0>; break;
+                case 192: kern = k_dec_xn_fast<1024, 192, ZR_DEC_T8 != 0>; break;
+                case 256: kern = k_dec_xn_fast<1024, 256, ZR_DEC_T8 != 0>; break;
+                case 512: kern = k_dec_xn_fast<1024, 512, ZR_DEC_T8 != 0>; break;
+                case 576: kern = k_dec_xn_fast<1024, 576, ZR_DEC_T8 != 0>; break;
                 default: break;
             }
 #else
-            auto kern = k_dec_xn_fast<1024, 0>;
+            auto kern = k_dec_xn_fast<1024, 0, ZR_DEC_T8 != 0>;
 #endif
             launch_timed("rans_decode", kern, dim3(nblkF * a.B), dim3(1024), 0, s, enc, raw, a, w, nblkF, epoch);
         }
