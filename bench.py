@@ -538,7 +538,7 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
     enc = bt.new_enc()
     out = bt.new_raw()
 
-    comm = zd.RcclComm(world, rank) if world > 1 else None  # the shared trained table over ranks
+    comm = zd.shared_table_comm(world, rank) if world > 1 else None  # the shared trained table over ranks
 
     def step():
         bt.histogram(raw)
@@ -626,7 +626,7 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
 
     # the shared frequency table over ranks: the library's own RCCL communicator
     # (zr_comm_*; the unique id travels over the torch process group, host side)
-    comm = zd.RcclComm(world, rank) if world > 1 else None
+    comm = zd.shared_table_comm(world, rank) if world > 1 else None
 
     # --groups G > 1: after the shared table, the B buffers are coded as G groups
     # of B / G on G streams (each group its own batch and workspace over the same

@@ -44,7 +44,14 @@ def _rank_main(rank, world, port, q):
         ot = O.rans_table(O.histogram(union))
         ref = list(ot.freq) + list(ot.start)
         t = zd.max_over_ranks(0.5 + rank)
-        q.put((rank, all(x == ref for x in tabs), t))
+        # the bench's communicator: no GPU here, so zr_comm cannot come up and
+        # every rank falls back to the process group together (no rank left in
+        # a collective init)
+        comm = zd.shared_table_comm(world, rank)
+        h2 = torch.tensor(np.bincount(np.frombuffer(shard, dtype=np.uint8), minlength=256).astype(np.int64))
+        comm.allreduce_histogram(h2)
+        comm.close()
+        q.put((rank, all(x == ref for x in tabs) and bool(torch.equal(h, h2)), t))
     finally:
         dist.destroy_process_group()
 

@@ -102,6 +102,52 @@ def exchange_id(rank):
     return obj[0]
 
 
+class TorchComm:
+    """The same exchange on torch.distributed's process group (RCCL for the
+    "nccl" backend): the fallback of `shared_table_comm`."""
+
+    def allreduce_histogram(self, hist, stream=None):
+        return allreduce_histogram(hist)
+
+    def close(self):
+        pass
+
+
+def shared_table_comm(nranks, rank):
+    """The shared-table communicator of a multi-rank run: the library's own
+    RCCL communicator (zr_comm_*), or, when it cannot be set up, the
+    torch.distributed group's (reported on stderr; the run goes on). The ranks
+    agree before any of them enters the collective init, so one rank's failure
+    cannot leave the others waiting in it."""
+    import sys
+    uid, err = None, None
+    if rank == 0:
+        try:
+            uid = RcclComm.unique_id()
+        except Exception as e:  # noqa: BLE001
+            err = e
+    obj = [uid]
+    dist.broadcast_object_list(obj, src=0)
+    uid = obj[0]
+    ok = torch.tensor([1 if uid is not None and hasattr(_lib_load(), "zr_comm_init") else 0], dtype=torch.int32)
+    if dist.get_backend() != "gloo":
+        ok = ok.cuda()
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 1:
+        try:
+            return RcclComm(nranks, rank, unique_id=uid)
+        except Exception as e:  # noqa: BLE001
+            err = e
+    print(f"zipora_amd: no zr_comm communicator ({err}); histogram all-reduce on torch.distributed",
+          file=sys.stderr)
+    return TorchComm()
+
+
+def _lib_load():
+    from . import _lib
+    return _lib.load()
+
+
 def max_over_ranks(seconds, device=None):
     """The bench contract's timing: the slowest rank's wall time."""
     t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
