@@ -685,7 +685,8 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     if comm is not None:
         comm.close()
     if diag:  # tools/*.sh read the kernel times; no metric from a diagnostic build
-        return {"diagnostic": diag, "kernels_ms": kms, "ms_per_step": round(dt / args.steps * 1e3, 4)}
+        return {"diagnostic": diag, "kernels_ms": kms, "ms_per_step": round(dt / args.steps * 1e3, 4),
+                "timed_ms": {k: round(v, 4) for k, v in tms.items()}}
     literal = B == 1
     wl = "rans_literal" if literal else "rans"
     rans_bytes = {"rans_encode": total + comp_bytes, "rans_decode": comp_bytes + total,

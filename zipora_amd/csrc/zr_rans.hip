@@ -416,12 +416,21 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 // workgroups (16 waves) per CU.
 // IL: the batch's scratch layout (RansWork::il), a template parameter so that
 // the long-stream (contiguous) instance keeps its constant addressing.
+#ifndef ZR_ENC_DB
+#define ZR_ENC_DB 1
+#endif
 template <uint32_t EW, int ABL, bool IL>
 __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
-    constexpr uint32_t ERS = 32;    // ring slots (dwords) per lane
-    constexpr uint32_t ETILE = 16;  // input rows (steps) per tile
+    // DB: two input tiles, written alternately, so one barrier per tile
+    // separates a tile's writes from its reads (the other barrier kept the
+    // next tile's writes from overtaking slow readers); the room comes from a
+    // 16-slot ring flushed in 32-B bursts (pending <= 7 + 8 dwords)
+    constexpr bool DB = ZR_ENC_DB != 0;
+    constexpr uint32_t ERS = DB ? 16 : 32;  // ring slots (dwords) per lane
+    constexpr uint32_t FL = ERS / 2;        // dwords per flush burst
+    constexpr uint32_t ETILE = 16;          // input rows (steps) per tile
     constexpr uint32_t RING_BYTES = ERS * EW * 4;  // a power of two
-    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16 + ETILE * EW];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16 + (DB ? 2 : 1) * ETILE * EW];
     uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
     uint4 *et = reinterpret_cast<uint4 *>(lds + RING_BYTES);
     uint8_t *itile = lds + RING_BYTES + 256 * 16;
@@ -542,26 +551,26 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     };
     auto nw_of = [&]() -> uint32_t { return nw32 >> 5; };
     auto flush64 = [&]() {  // tile boundary: at most one 64-B burst per lane
-        const bool need = nw_of() - nfl >= 16;
+        const bool need = nw_of() - nfl >= FL;
         {
             if (need) {
-                // nfl is a multiple of 16: the 16 dwords are ring rows
-                // (nfl & 16) .. +15, one base address and immediate offsets
-                const uint32_t *r = ring + (nfl & 16) * EW + tid;
-                uint32_t d[16];
+                // nfl is a multiple of FL: the FL dwords are ring rows
+                // (nfl & FL) .. +FL-1, one base address and immediate offsets
+                const uint32_t *r = ring + (nfl & FL) * EW + tid;
+                uint32_t d[FL];
 #pragma unroll
-                for (int i = 0; i < 16; i++) d[i] = r[i * EW];
+                for (int i = 0; i < (int)FL; i++) d[i] = r[i * EW];
                 const uint32_t o = nfl >> 2;
                 if (!(ABL & 1)) {
                     v4u *q0 = quad(o);
-                    *q0 = v4u{d[0], d[1], d[2], d[3]};
-                    *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + qstride) = v4u{d[4], d[5], d[6], d[7]};
-                    *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + 2 * qstride) = v4u{d[8], d[9], d[10], d[11]};
-                    *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + 3 * qstride) = v4u{d[12], d[13], d[14], d[15]};
+#pragma unroll
+                    for (int k = 0; k < (int)FL / 4; k++)
+                        *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + k * qstride) =
+                            v4u{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
                 } else {
-                    asm volatile("" ::"v"(d[0]), "v"(d[15]));
+                    asm volatile("" ::"v"(d[0]), "v"(d[FL - 1]));
                 }
-                nfl += 16;
+                nfl += FL;
             }
         }
     };
@@ -578,11 +587,11 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         return v4u{v.x, v.y, v.z, v.w};
     };
     // one full tile, rows ETILE-1 .. 0, every lane a stream with all rows valid
-    auto tile_fast = [&]() {
+    auto tile_fast = [&](const uint8_t *tl) {
 #pragma unroll
         for (int g = ETILE - 4; g >= 0; g -= 4) {
-            uint32_t s3 = itile[(g + 3) * EW + tid], s2 = itile[(g + 2) * EW + tid];
-            uint32_t s1 = itile[(g + 1) * EW + tid], s0 = itile[g * EW + tid];
+            uint32_t s3 = tl[(g + 3) * EW + tid], s2 = tl[(g + 2) * EW + tid];
+            uint32_t s1 = tl[(g + 1) * EW + tid], s0 = tl[g * EW + tid];
             if (ABL & 2) {  // diagnostic: conflict-free table reads (consecutive entries)
                 const uint32_t t = (tid + (s0 & 1)) & 255;
                 s3 = s2 = s1 = s0 = t;
@@ -620,8 +629,9 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         }
     };
     for (uint64_t t = ntiles; t-- > 0;) {
-        tile_sync();
-        *reinterpret_cast<v4u *>(&itile[lr * EW + lp]) = pend;
+        uint8_t *const tl = itile + (DB ? (uint32_t)(t & 1) * ETILE * EW : 0u);
+        if (!DB) tile_sync();
+        *reinterpret_cast<v4u *>(&tl[lr * EW + lp]) = pend;
         tile_sync();
         if (body_ok && t >= 2)  // (non-temporal: same-box A/B 0.244 -> 0.238 ms)
             pend = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(inb + ((t - 1) * ETILE + lr) * N + col));
@@ -630,13 +640,13 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         flush64();
         const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
         if (rtop == ETILE && t * ETILE + ETILE < cmax && wave_all) {
-            tile_fast();
+            tile_fast(tl);
         } else {
             // general tile: rows past a stream's end or lanes without a stream
             // leave the state and emit nothing
             for (uint32_t r = rtop; r-- > 0;) {
                 const uint64_t k = t * ETILE + r;
-                const uint32_t sym = itile[r * EW + tid];
+                const uint32_t sym = tl[r * EW + tid];
                 const uint4 e = et[sym];
                 const bool valid = active && k < c;
                 err |= valid && e.x == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
