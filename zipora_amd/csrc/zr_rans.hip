@@ -1279,22 +1279,25 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     uint32_t *flag = ring + 64;
     const uint32_t tid = threadIdx.x;
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
-    {
-        const v4u *src = reinterpret_cast<const v4u *>(T->slot);
-        v4u *dst = reinterpret_cast<v4u *>(lds);
-        if (WT) {
-            for (uint32_t j = tid; j < TOTFREQ / 4; j += FW) {
-                const v4u q = src[j];
-                auto wide = [](uint32_t e) -> v2u { return v2u{(e >> 20) | (e << 24), (e >> 8) & 0xFFF}; };
-                const v2u w0 = wide(q.x), w1 = wide(q.y), w2 = wide(q.z), w3 = wide(q.w);
-                dst[2 * j] = v4u{w0.x, w0.y, w1.x, w1.y};
-                dst[2 * j + 1] = v4u{w2.x, w2.y, w3.x, w3.y};
-            }
-        } else {
-            for (uint32_t j = tid; j < TOTFREQ / 4; j += FW) dst[j] = src[j];
-        }
-    }
+    // the prologue's global loads (slot table, table kind, this lane's state,
+    // the stream lengths) do not depend on each other: they are all issued
+    // before the first use of any, one memory round trip instead of one each
+    const v4u *tsrc = reinterpret_cast<const v4u *>(T->slot);
+    constexpr bool TQ1 = FW >= TOTFREQ / 4;  // one table word per lane at most
+    v4u tq = {0, 0, 0, 0};
+    if (TQ1 && tid < TOTFREQ / 4) tq = tsrc[tid];
+    const uint32_t kind = T->kind;
     const uint8_t *e = enc + a.enc_off[b];
+    const uint32_t s = blkF * FW + tid;
+    const bool active = s < N;
+    // min_header_size (rans.rs:563-568): epoch mode checks it here, before any
+    // stream read; otherwise k_dec_hdr did
+    const bool hdr_ok = !epoch || a.enc_len[b] >= (uint64_t)N * 12;
+    uint64_t X = RANS_L;
+    if (active && hdr_ok) {
+        const uint8_t *px = e + 8 * (size_t)s;
+        X = (((uintptr_t)e) & 7) == 0 ? *reinterpret_cast<const uint64_t *>(px) : ld_u64_u(px);
+    }
     const bool len4 = ((((uintptr_t)e) | N) & 3) == 0;  // the length array is dword-aligned
     auto stream_len = [&](uint32_t i) -> uint32_t {
         const uint8_t *p = e + 8 * (size_t)N + 4 * (size_t)i;
@@ -1302,20 +1305,29 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     };
     // blo: the bytes of the buffer's streams below this workgroup's first one
     uint64_t blo;
-    uint32_t own_len = 0;  // (epoch mode: this lane's stream length, read with the others)
+    // this lane's stream length (epoch mode: own_len, read with the others)
+    const uint32_t own_hdr = !epoch && active ? stream_len(s) : 0u;
+    uint32_t own_len = 0;
     if (epoch) {
-        // min_header_size (rans.rs:563-568), then "Invalid stream data length"
-        // (rans.rs:608-610), before any stream read
-        const bool hdr_ok = a.enc_len[b] >= (uint64_t)N * 12;
+        // "Invalid stream data length" (rans.rs:608-610)
         const uint32_t first = blkF * FW;
         uint64_t lo = 0, tot = 0;
         if (hdr_ok) {
-            for (uint32_t i = tid; i < N; i += FW) {
-                const uint32_t v = stream_len(i);
+            auto acc = [&](uint32_t i, uint32_t v) __attribute__((always_inline)) {
                 tot += v;
                 lo += i < first ? v : 0u;
                 own_len = i == first + tid ? v : own_len;
+            };
+            uint32_t i = tid;
+            for (; i + 3 * FW < N; i += 4 * FW) {  // four loads in flight per lane
+                const uint32_t v0 = stream_len(i), v1 = stream_len(i + FW), v2 = stream_len(i + 2 * FW),
+                               v3 = stream_len(i + 3 * FW);
+                acc(i, v0);
+                acc(i + FW, v1);
+                acc(i + 2 * FW, v2);
+                acc(i + 3 * FW, v3);
             }
+            for (; i < N; i += FW) acc(i, stream_len(i));
         }
         lo = wave_sum(lo);
         tot = wave_sum(tot);
@@ -1363,10 +1375,25 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
                 __builtin_amdgcn_s_sleep(8);
         a.status[b] = ZR_INVALID_INPUT;
     };
-    const uint32_t kind = T->kind;
-    const uint32_t s = blkF * FW + tid;
-    const bool active = s < N;
-    const uint32_t L = !active ? 0u : epoch ? own_len : stream_len(s);
+    {  // the slot table into LDS (before the barrier below)
+        v4u *dst = reinterpret_cast<v4u *>(lds);
+        auto put = [&](uint32_t j, const v4u q) __attribute__((always_inline)) {
+            if (WT) {
+                auto wide = [](uint32_t e) -> v2u { return v2u{(e >> 20) | (e << 24), (e >> 8) & 0xFFF}; };
+                const v2u w0 = wide(q.x), w1 = wide(q.y), w2 = wide(q.z), w3 = wide(q.w);
+                dst[2 * j] = v4u{w0.x, w0.y, w1.x, w1.y};
+                dst[2 * j + 1] = v4u{w2.x, w2.y, w3.x, w3.y};
+            } else {
+                dst[j] = q;
+            }
+        };
+        if (TQ1) {
+            if (tid < TOTFREQ / 4) put(tid, tq);
+        } else {
+            for (uint32_t j = tid; j < TOTFREQ / 4; j += FW) put(j, tsrc[j]);
+        }
+    }
+    const uint32_t L = !active ? 0u : epoch ? own_len : own_hdr;
     const unsigned long long inc = wave_incl_scan(L);
     const int wv = tid >> 6;
     if ((tid & 63) == 63) sh[wv] = inc;
@@ -1384,7 +1411,6 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         sub = wave_sum(v);  // FW < 256 is one wave
     }
     const uint64_t off = base + inc - L + blo + sub;
-    const uint64_t X = active ? ld_u64_u(e + 8 * (size_t)s) : RANS_L;
     const bool fast = kind == DT_NORMAL && X >= RANS_L && X < (1ull << 24);
     if (!fast) atomicOr(flag, 1u);
     __syncthreads();
