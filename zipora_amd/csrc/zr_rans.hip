@@ -883,7 +883,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     };
     // the group's streams: offsets, lengths, header words, first window's chunk
     // ranges (lanes [l0, l0 + ns) of the calling wave hold streams s0 ..)
-    auto group_setup = [&](bool mine, uint32_t i, uint32_t sb, uint64_t off, uint32_t L, uint32_t l0) {
+    auto group_setup = [&](bool mine, uint32_t i, uint32_t sb, uint64_t off, uint32_t L, uint32_t X, uint32_t l0) {
         const uint64_t g_r0 = __shfl(off, (int)l0, 64);
         const uint64_t g_r1 = __shfl(off + L, (int)(l0 + ns - 1), 64);
         const uintptr_t g_ua0 = ((uintptr_t)dbase + g_r0) & ~(uintptr_t)15;
@@ -891,8 +891,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         if (mine) {
             soff[i] = off;
             slen[i] = L;
-            if (wi == 0) {
-                const uint32_t X = w.st_state[(size_t)b * N + sb];
+            if (wi == 0) {  // (X: the stream's final state, st_state)
                 uint8_t *e = enc + a.enc_off[b];
                 if ((((uintptr_t)e) & 7) == 0) {
                     *reinterpret_cast<uint2 *>(e + 8 * (size_t)sb) = make_uint2(X, 0);
@@ -916,7 +915,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         // up, one barrier, no block scan
         __shared__ uint32_t sfail;
         if (wv == 0) {
+            // every load of the setup issued at once (one memory round trip): the
+            // block sums, and the group's lengths, offsets and (first window)
+            // final states, used only if no block is flagged
             const uint64_t v = lane < nblk ? w.blocksum[(size_t)b * nblk + lane] : 0;
+            const bool mine = lane < ns;
+            const uint32_t sb = s0 + lane;
+            const uint32_t L = mine ? w.st_len[(size_t)b * N + sb] : 0;
+            const uint32_t o32 = mine ? w.st_off[(size_t)b * N + sb] : 0;
+            const uint32_t X = mine && wi == 0 ? w.st_state[(size_t)b * N + sb] : 0;
             const uint64_t c = v & ~BS_ERR;
             const uint64_t below = wave_sum(lane < blk ? c : 0);
             const bool flagged = __any((v >> 63) != 0);
@@ -927,13 +934,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                     a.status[b] = flagged ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an xN encode
                 }
             }
-            if (!flagged) {
-                const bool mine = lane < ns;
-                const uint32_t sb = s0 + lane;
-                const uint32_t L = mine ? w.st_len[(size_t)b * N + sb] : 0;
-                const uint64_t off = mine ? (uint64_t)w.st_off[(size_t)b * N + sb] + below : 0;
-                group_setup(mine, lane, sb, off, L, 0);
-            }
+            if (!flagged) group_setup(mine, lane, sb, mine ? (uint64_t)o32 + below : 0, L, X, 0);
             if (lane == 0) sfail = flagged;
         }
         __syncthreads();
@@ -983,7 +984,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         const uint32_t L = sb < N ? w.st_len[(size_t)b * N + sb] : 0;
         const uint64_t off = block_excl_scan(L, sh, nullptr) + bo;
         const uint32_t l0 = (s0 - blk * 256) & 63;
-        if (wv == (s0 - blk * 256) / 64) group_setup(mine, i, sb, off, L, l0);  // the group's wave (uniform branch)
+        if (wv == (s0 - blk * 256) / 64) {  // the group's wave (uniform branch)
+            const uint32_t X = mine && wi == 0 ? w.st_state[(size_t)b * N + sb] : 0;
+            group_setup(mine, i, sb, off, L, X, l0);
+        }
     }
     __syncthreads();
     }
