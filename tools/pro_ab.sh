@@ -6,4 +6,4 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_fastpath_gpu.py tests/test_rans_gpu.py tests/test_rans_r02_gpu.py -m gpu -x -q --timeout 170 --timeout-method thread > gpurun_out/pro_tests.log 2>&1 && \
-bash tools/ab_multi.sh "zipora_amd/ab/lib_base.so zipora_amd/ab/lib_${1:-var}.so"
+bash tools/ab_multi.sh "zipora_amd/ab/lib_base.so $(for v in ${@:-var}; do echo -n "zipora_amd/ab/lib_$v.so "; done)"
