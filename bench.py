@@ -26,7 +26,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks, one process per GPU. Without WORLD_SIZE in the environment and N > 1, "
+                        "bench.py starts the N rank processes itself; under torchrun it must equal WORLD_SIZE")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--buffers", type=int, default=64)
@@ -46,6 +48,9 @@ def parse():
                         "(encode+compaction+decode of one group overlap the others')")
     p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--fse-block-kib", type=int, default=64)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher check without a GPU: the ranks join a gloo group, time an empty step and "
+                        "rank 0 prints the rank count (no kernels, no metric)")
     return p.parse_args()
 
 
@@ -437,6 +442,17 @@ def _timed(torch, dist, world, dev, fn, steps, warmup, timer=None):
     return zd.max_over_ranks(time.perf_counter() - t0, dev)
 
 
+def _exchange_info(zd, comm, world):
+    """How the shared table's histogram crossed the ranks: RCCL's own rank count
+    of the library communicator (ncclCommCount via zr_comm_count), or the
+    torch.distributed fallback, or none (one rank)."""
+    if comm is None:
+        return {"rccl_ranks": None, "histogram_exchange": "none (one rank)"}
+    if isinstance(comm, zd.RcclComm):
+        return {"rccl_ranks": comm.count(), "histogram_exchange": "zr_comm (RCCL all-reduce, u32 SUM)"}
+    return {"rccl_ranks": None, "histogram_exchange": "torch.distributed all_reduce (zr_comm unavailable)"}
+
+
 def _line(metric, value, world, args, dt, data, config, roofline, extra):
     r = {"metric": metric, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
          "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
@@ -477,11 +493,11 @@ def cpu_baseline_blob(host, threads):
     per = 4096
     nrec = min(len(host) // 1024, per * threads)
     t = _table_fast(O, host[:nrec * 1024])
+    buf = bytes(host[:nrec * 1024])
 
-    def one(k):
-        for r in range(k * per, min(nrec, (k + 1) * per)):
-            d = host[r * 1024:(r + 1) * 1024]
-            assert O.rans_decode(t, 1, O.rans_encode(t, 1, d), 1024) == d
+    def one(k):  # a whole record group per oracle call: the C loop runs without the GIL
+        lo = k * per
+        O.rans_x1_records(t, buf, lo * 1024, min(nrec, lo + per) - lo, 1024)
 
     dt, passes = _cpu_repeat(one, range((nrec + per - 1) // per), threads)
     dt1, p1 = _cpu_repeat(one, range(1), 1)
@@ -493,6 +509,66 @@ def cpu_baseline_blob(host, threads):
                               "kind": "port",
                               "sample": f"{p1} passes over {per} x 1 KiB records, x1 encode+decode, shared table, "
                                         f"{dt1:.2f} s wall"}}
+
+
+PUBLISHED_O0 = {"value_mbps": {"entropy 0.5": 58.3, "entropy 2.0": 53.1, "entropy 6.0": 38.1},
+                "what": "HuffmanEncoder::new + encode, 64 KiB, 1 thread, AMD EPYC 7B13 (Zen 3), rustc 1.91.1",
+                "source": "docs/PERFORMANCE.md:77 (benches/entropy_bench.rs:48-59)"}
+
+
+def huffman_o0_line(zr, L=None):
+    """BASELINE configs[0]: HuffmanEncoder O0 encode+decode of 1 MiB synthetic bytes
+    on the CPU reference path (examples/entropy_coding_demo.rs:36-65): the oracle's
+    restatement of tree.rs/encoder.rs/decoder.rs (bit-serial pack, tree walk), one
+    thread, on text-like (`t`) and uniform (`u`) bytes, printed beside the
+    reference's published encode rate (docs/PERFORMANCE.md:77, 64 KiB). The same
+    calls through the library's host API (tree on the host, kernels on the GPU,
+    H2D/D2H included) are shown beside it, checked byte for byte."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    O.lib()
+    out = {"metric": "MB/s Huffman O0 encode+decode, 1 MiB, CPU reference path (configs[0])", "unit": "MB/s",
+           "published_reference": PUBLISHED_O0, "inputs": {}}
+
+    def rate(fn, nbytes, min_s=1.0):
+        k, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            k += 1
+            dt = time.perf_counter() - t0
+            if dt >= min_s:
+                return round(k * nbytes / dt / 1e6, 2)
+
+    for kind in ("t", "u"):
+        row = {}
+        for n in (1 << 20, 1 << 16):
+            d = zr.synth(kind, n, seed=0x9E3779B97F4A7C15)
+            t = O.huff_tree(O.histogram(d))
+            enc = O.huff_encode(t, d)
+            assert O.huff_decode(t, enc, n) == d
+            r = {"encode_incl_tree_mbps": rate(lambda: O.huff_encode(O.huff_tree(O.histogram(d)), d), n),
+                 "decode_mbps": rate(lambda: O.huff_decode(t, enc, n), n),
+                 "encode_decode_mbps": rate(lambda: O.huff_decode(t, O.huff_encode(O.huff_tree(O.histogram(d)),
+                                                                                   d), n), n),
+                 "bits_per_byte": round(8 * len(enc) / n, 4)}
+            if n == 1 << 20:
+                he = zr.HuffmanEncoder(d)
+                g = he.encode(d)
+                assert g == enc, "GPU Huffman O0 differs from the oracle"
+                dec = zr.HuffmanDecoder(he.tree())
+                assert dec.decode(g, n) == d
+                r["gpu_host_api_encode_decode_mbps"] = rate(
+                    lambda: zr.HuffmanDecoder(zr.HuffmanEncoder(d).tree()).decode(zr.HuffmanEncoder(d).encode(d),
+                                                                                   n), n)
+            row[f"{n >> 10}KiB"] = r
+        out["inputs"][kind] = row
+    out["value"] = out["inputs"]["t"]["1024KiB"]["encode_decode_mbps"]
+    out["cpu_baseline"] = {"value": out["value"], "unit": "MB/s", "cores": 1, "kind": "port",
+                           "sample": "1 MiB of text-like bytes, tree build + encode + decode, >= 1 s of repeats"}
+    out["note"] = ("configs[0] is the CPU plumbing case (no GPU in the reference's path); "
+                   "gpu_host_api_* is zr_huff_encode/zr_huff_decode from host memory, the tree built twice "
+                   "per round trip as the Python mirror does")
+    return out
 
 
 def run_o1(args, torch, dist, world, rank, dev, zr, L):
@@ -549,12 +625,15 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
         bt.decode(enc, out)
 
     dt, dom, dom_ms, kms, _ = _measure(torch, dist, world, dev, L, step, args, ["rans_decode_x1", "rans_encode_x1"])
+    exch = _exchange_info(zd, comm, world)
+    if comm is not None:
+        comm.close()
     bt.raise_on_error()
     if not torch.equal(out, raw):
         raise SystemExit("blob round trip mismatch")
     comp = int(bt.enc_len.sum().item())
     extra = {"kernels_ms": kms, "kernels_ms_source": KMS_SOURCE,
-             "compressed_bytes": comp, "ratio": round(comp / total, 5)}
+             "compressed_bytes": comp, "ratio": round(comp / total, 5), **exch}
     if world == 1 and not args.no_host_path:
         extra.update(host_pipe_rates(zr, bt, host, [1024] * R, 1, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -564,7 +643,7 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
                  {"workload": f"{R} x 1 KiB records per GPU, rANS x1 per record, shared trained table",
                   "records": R, "parallelism": f"shard{world}"},
                  _roofline(dom, dom_ms, {"rans_decode_x1": comp + total, "rans_encode_x1": total + comp}, "blob",
-                           {"rans_decode_x1": "k_dec_x1_fast", "rans_encode_x1": "k_enc_x1_fast"}), extra)
+                           {"rans_decode_x1": "k_dec_x1_fast", "rans_encode_x1": "k_enc_x1_ring"}), extra)
 
 
 
@@ -682,6 +761,7 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     else:
         comp_bytes = int(bt.enc_len.sum().item())
     value = world * total * args.steps / dt / 2**30
+    exch = _exchange_info(zd, comm, world)
     if comm is not None:
         comm.close()
     if diag:  # tools/*.sh read the kernel times; no metric from a diagnostic build
@@ -723,6 +803,7 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
         "compressed_bytes": comp_bytes,
         "ratio": round(comp_bytes / total, 5),
     }
+    res.update(exch)
     if rank == 0 and world == 1 and host_path and not args.no_host_path:
         res.update(host_pipe_rates(zr, bt, host[:total], [n] * B, N, args.steps))
     if rank == 0 and world == 1 and cpu and not args.no_cpu_baseline:
@@ -735,14 +816,17 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
 
 SECONDARY_KEYS = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "config", "roofline",
                   "roofline_decode", "kernels_ms", "compressed_bytes", "ratio", "cpu_baseline",
-                  "host_resident_gibps", "host_encode_gibps", "host_decode_gibps")
+                  "host_resident_gibps", "host_encode_gibps", "host_decode_gibps", "rccl_ranks",
+                  "histogram_exchange")
 
 
 def secondary_lines(args, torch, dist, world, rank, dev, zr, L, host):
-    """The other BASELINE configs in the default run, each a
-    short run of its own workload: configs[1] as written (one 256 MiB buffer x
-    4096 streams), configs[2] (FSE, 64 KiB blocks), configs[4] (the 1 M x 1 KiB
-    record batch). Not part of `value`."""
+    """The other BASELINE configs in the default run,
+    each a short run of its own workload: configs[1] as written (one 256 MiB
+    buffer x 4096 streams), configs[2] (FSE, 64 KiB blocks), configs[4] (the
+    1 M x 1 KiB record batch), configs[3] (Huffman O1, the 128 MiB per-GPU shard
+    of 1 GiB) and configs[0] (Huffman O0, 1 MiB, the CPU reference path). Not
+    part of `value`."""
     import copy
     out = {}
 
@@ -765,11 +849,81 @@ def secondary_lines(args, torch, dist, world, rank, dev, zr, L, host):
     a.records = 1 << 20
     out["blob"] = slim(run_blob(a, torch, dist, world, rank, dev, zr, L))
     torch.cuda.empty_cache()
+    out["o1"] = slim(run_o1(sub(5, 2), torch, dist, world, rank, dev, zr, L))
+    torch.cuda.empty_cache()
+    if not args.no_cpu_baseline:
+        out["huffman_o0"] = huffman_o0_line(zr)
     return out
+
+
+def launch(args):
+    """--gpus N > 1 without a launcher: start N rank processes (RANK/LOCAL_RANK/
+    WORLD_SIZE/MASTER_* set as torch.distributed.run sets them, MASTER_ADDR
+    127.0.0.1) as children of this process, which never touches a GPU; wait for
+    them and exit with the first failure's code (the others are stopped). Only
+    rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    n = args.gpus
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc, alive = 0, set(range(n))
+    while alive:
+        for i in sorted(alive):
+            c = procs[i].poll()
+            if c is None:
+                continue
+            alive.discard(i)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py: rank {i} exited with {c}; stopping the other ranks", file=sys.stderr)
+                for j in alive:
+                    procs[j].terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def dry_run(world, rank):
+    """The launcher path on a CPU box: a gloo group of `world` ranks, one empty
+    timed step under the contract's barrier + max-over-ranks timing."""
+    import torch
+    import torch.distributed as dist
+    from zipora_amd import dist as zd
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    dt = zd.max_over_ranks(time.perf_counter() - t0)
+    seen = [(rank, os.getpid())]
+    if world > 1:
+        seen = [None] * world
+        dist.all_gather_object(seen, (rank, os.getpid()))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": [r for r, _ in seen],
+                          "processes": len({p for _, p in seen}),
+                          "backend": dist.get_backend() if world > 1 else None, "max_s": dt}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch(args))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    if args.dry_run:
+        return dry_run(int(env_world or 1), int(os.environ.get("RANK", "0")))
     from zipora_amd import _lib as _zl
     diag = _zl.diag_env()  # profiling ablations: garbage output, never a metric line
     import torch

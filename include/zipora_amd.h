@@ -289,6 +289,8 @@ typedef struct zr_comm zr_comm;
 int32_t zr_comm_unique_id(uint8_t id[ZR_COMM_ID_BYTES]);
 /* collective over nranks processes; binds the calling thread's current device */
 int32_t zr_comm_init(const uint8_t id[ZR_COMM_ID_BYTES], int32_t nranks, int32_t rank, zr_comm **comm);
+/* the number of ranks RCCL itself reports for the communicator (ncclCommCount) */
+int32_t zr_comm_count(const zr_comm *comm, int32_t *nranks);
 /* in-place u32 SUM of n_bins device counters over the ranks (wraps mod 2^32 per
  * bin, as the reference's u32 counts); stream-ordered */
 int32_t zr_histogram_allreduce_dev(zr_comm *comm, uint32_t *hist_dev, uint32_t n_bins, void *stream);

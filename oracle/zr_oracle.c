@@ -1591,6 +1591,35 @@ int or_ctx_decode(const or_ctx_huff *c, const uint8_t *in, size_t in_len, uint8_
 }
 
 /* ======================================================================== */
+/* record groups (bench.py's configs[4] CPU baseline)                        */
+/* ======================================================================== */
+/* Each of n_rec records of rec_len bytes at in + r*rec_len: Rans64Encoder::<X1>
+ * encode (rans.rs:354-366) then decode (rans.rs:523-552) with the one shared
+ * table, the round trip checked; the per-record codec RansBlobStore /
+ * RansCompressor run (compression/mod.rs:456-517). One call per record group,
+ * so a caller's threads do not meet on the interpreter lock per record.
+ * *enc_total = the records' encoded bytes. -1 if any record fails to round-trip. */
+int or_rans_x1_records(const or_rans_table *t, const uint8_t *in, size_t n_rec, size_t rec_len,
+                       size_t *enc_total) {
+    size_t cap = or_rans_encode_bound(rec_len, 1);
+    uint8_t *enc = (uint8_t *)malloc(cap ? cap : 1), *dec = (uint8_t *)malloc(rec_len ? rec_len : 1);
+    size_t tot = 0;
+    int st = (enc && dec) ? OK : -2;
+    for (size_t r = 0; st == OK && r < n_rec; r++) {
+        const uint8_t *d = in + r * rec_len;
+        size_t el = 0;
+        st = or_rans_encode(t, 1, d, rec_len, enc, &el);
+        if (st == OK) st = or_rans_decode(t, 1, enc, el, dec, rec_len);
+        if (st == OK && memcmp(dec, d, rec_len) != 0) st = EINVAL_DATA;
+        tot += el;
+    }
+    free(enc);
+    free(dec);
+    if (enc_total) *enc_total = tot;
+    return st;
+}
+
+/* ======================================================================== */
 /* inputs                                                                    */
 /* ======================================================================== */
 void or_gen_uniform(uint64_t seed, uint8_t *out, size_t n) { /* tests/fse_tests.rs:711-717 */

@@ -115,6 +115,11 @@ int or_ctx_decode(const or_ctx_huff *c, const uint8_t *in, size_t in_len, uint8_
 int or_ctx_decode_xn(const or_ctx_huff *c, int nway, const uint8_t *in, size_t in_len, uint8_t *out,
                      size_t n, size_t *out_len);
 
+/* ---- record groups: x1 encode+decode of n_rec records of rec_len bytes with
+ * one table, round trip checked; *enc_total = encoded bytes (bench CPU leg) ---- */
+int or_rans_x1_records(const or_rans_table *t, const uint8_t *in, size_t n_rec, size_t rec_len,
+                       size_t *enc_total);
+
 /* ---- deterministic inputs ---- */
 void or_gen_uniform(uint64_t seed, uint8_t *out, size_t n); /* tests/fse_tests.rs:711-717 */
 

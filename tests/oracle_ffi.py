@@ -90,6 +90,7 @@ def lib():
         L.or_ctx_decode_xn.argtypes = [ctypes.c_void_p, ctypes.c_int, u8p, sz, u8p, sz,
                                        ctypes.POINTER(sz)]
         L.or_gen_uniform.argtypes = [ctypes.c_uint64, u8p, sz]
+        L.or_rans_x1_records.argtypes = [ctypes.POINTER(RansTable), ctypes.c_void_p, sz, sz, ctypes.POINTER(sz)]
         _lib = L
     return _lib
 
@@ -414,6 +415,18 @@ class Ctx:
         ol = sz(0)
         _check(lib().or_ctx_decode_xn(self.h, nway, b, ln, out, n, ctypes.byref(ol)), "ctx_decode_xn")
         return ctypes.string_at(out, ol.value)
+
+
+def rans_x1_records(table, buf, offset, n_rec, rec_len):
+    """x1 encode+decode of n_rec records of rec_len bytes of `buf` (a bytes-like
+    object kept alive by the caller) starting at `offset`, one C call (the GIL is
+    released for the whole group). Returns the encoded byte total."""
+    base = ctypes.addressof(ctypes.c_char.from_buffer(buf)) if isinstance(buf, bytearray) else \
+        ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value
+    tot = sz(0)
+    _check(lib().or_rans_x1_records(ctypes.byref(table), base + offset, n_rec, rec_len, ctypes.byref(tot)),
+           "rans_x1_records")
+    return tot.value
 
 
 def gen_uniform(n, seed=0x9E3779B97F4A7C15):

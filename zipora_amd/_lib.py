@@ -77,6 +77,7 @@ SIGNATURES = [
     ("zr_rans_selftest_reciprocal", ctypes.c_int32, [c_u64p]),
     ("zr_comm_unique_id", ctypes.c_int32, [c_u8p]),
     ("zr_comm_init", ctypes.c_int32, [c_u8p, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(c_vp)]),
+    ("zr_comm_count", ctypes.c_int32, [c_vp, c_i32p]),
     ("zr_histogram_allreduce_dev", ctypes.c_int32, [c_vp, c_vp, ctypes.c_uint32, c_vp]),
     ("zr_table_broadcast_dev", ctypes.c_int32, [c_vp, c_vp, ctypes.c_uint32, ctypes.c_int32, c_vp]),
     ("zr_comm_destroy", ctypes.c_int32, [c_vp]),

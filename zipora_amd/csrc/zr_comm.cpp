@@ -33,6 +33,7 @@ struct Rccl {
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclBroadcast) broadcast = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
     std::string err;
 };
 
@@ -60,8 +61,9 @@ Rccl *rccl() {
         r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(sym("ncclAllReduce"));
         r.broadcast = reinterpret_cast<decltype(r.broadcast)>(sym("ncclBroadcast"));
         r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
+        r.comm_count = reinterpret_cast<decltype(r.comm_count)>(sym("ncclCommCount"));
         if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.broadcast ||
-            !r.error_string)
+            !r.error_string || !r.comm_count)
             r.err = "librccl lacks an entry point";
     });
     return r.err.empty() ? &r : nullptr;
@@ -116,6 +118,21 @@ int32_t zr_comm_init(const uint8_t id[ZR_COMM_ID_BYTES], int32_t nranks, int32_t
     const ncclResult_t e = r->comm_init_rank(&c, nranks, u, rank);  // collective over the ranks
     if (e != ncclSuccess) return rccl_fail(r, e, "ncclCommInitRank");
     *comm = new zr_comm{c, nranks, rank, dev};
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_comm_count(const zr_comm *comm, int32_t *nranks) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!comm || !nranks) return set_error(ZR_INVALID_INPUT, "null argument");
+    *nranks = 0;
+    Rccl *r = rccl();
+    if (!r) return rccl_missing();
+    int n = 0;  // RCCL's own view of the communicator, not the count the caller passed
+    const ncclResult_t e = r->comm_count(comm->comm, &n);
+    if (e != ncclSuccess) return rccl_fail(r, e, "ncclCommCount");
+    *nranks = n;
     return ZR_OK;
     ZR_GUARD_END
 }

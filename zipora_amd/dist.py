@@ -70,11 +70,22 @@ class RcclComm:
         return bytes(buf)
 
     def allreduce_histogram(self, hist, stream=None):
-        """In-place u32 SUM over the ranks of a device histogram (int32/uint32 tensor)."""
+        """In-place u32 SUM over the ranks of a device histogram (int32/uint32 tensor:
+        the RCCL call reduces numel() u32 counters, so any other dtype is refused)."""
+        if hist.dtype not in (torch.int32, torch.uint32) or not hist.is_contiguous() or not hist.is_cuda:
+            raise TypeError(f"RcclComm.allreduce_histogram needs a contiguous int32/uint32 device tensor, "
+                            f"got {hist.dtype} on {hist.device}")
         if stream is None:
             stream = torch.cuda.current_stream(hist.device).cuda_stream
         self._check(self._L.zr_histogram_allreduce_dev(self._h, hist.data_ptr(), hist.numel(), stream))
         return hist
+
+    def count(self):
+        """RCCL's own rank count of the communicator (ncclCommCount)."""
+        import ctypes
+        n = ctypes.c_int32(0)
+        self._check(self._L.zr_comm_count(self._h, ctypes.byref(n)))
+        return int(n.value)
 
     def broadcast_tables(self, tables, n_tables, root=0, stream=None):
         if stream is None:
@@ -115,10 +126,12 @@ class TorchComm:
 
 def shared_table_comm(nranks, rank):
     """The shared-table communicator of a multi-rank run: the library's own
-    RCCL communicator (zr_comm_*), or, when it cannot be set up, the
-    torch.distributed group's (reported on stderr; the run goes on). The ranks
-    agree before any of them enters the collective init, so one rank's failure
-    cannot leave the others waiting in it."""
+    RCCL communicator (zr_comm_*), or, when it cannot be set up on every rank,
+    the torch.distributed group's on every rank (reported on stderr; the run
+    goes on). The ranks agree twice: before the collective init (a rank that
+    has no id or no zr_comm keeps every rank out of it) and after it (a rank
+    whose init failed makes every rank destroy its communicator and fall back
+    together, so no two ranks run the exchange on different collectives)."""
     import sys
     uid, err = None, None
     if rank == 0:
@@ -129,18 +142,30 @@ def shared_table_comm(nranks, rank):
     obj = [uid]
     dist.broadcast_object_list(obj, src=0)
     uid = obj[0]
-    ok = torch.tensor([1 if uid is not None and hasattr(_lib_load(), "zr_comm_init") else 0], dtype=torch.int32)
-    if dist.get_backend() != "gloo":
-        ok = ok.cuda()
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    if int(ok.item()) == 1:
+    ok = 1 if uid is not None and hasattr(_lib_load(), "zr_comm_init") else 0
+    comm = None
+    if _all_ranks(ok):
         try:
-            return RcclComm(nranks, rank, unique_id=uid)
+            comm = RcclComm(nranks, rank, unique_id=uid)
         except Exception as e:  # noqa: BLE001
             err = e
+        if _all_ranks(1 if comm is not None else 0):
+            return comm
+        if comm is not None:
+            comm.close()
+            err = err or "another rank's zr_comm_init failed"
     print(f"zipora_amd: no zr_comm communicator ({err}); histogram all-reduce on torch.distributed",
           file=sys.stderr)
     return TorchComm()
+
+
+def _all_ranks(flag):
+    """True on every rank iff flag is true on every rank (all_reduce MIN on the group)."""
+    t = torch.tensor([int(bool(flag))], dtype=torch.int32)
+    if dist.get_backend() != "gloo":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item()) == 1
 
 
 def _lib_load():
