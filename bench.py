@@ -722,11 +722,18 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
             groups.append((sub, raw[lo:hi], enc[eo:], out[lo:hi], torch.cuda.Stream(dev)))
         ev_tab = torch.cuda.Event()
 
+    # one rank: histogram and table in one launch (the table built by the last
+    # histogram workgroup); more ranks: the all-reduce sits between the two
+    fused = comm is None and hasattr(L, "zr_rans_dtab_from_data_dev")
+
     def step():
-        bt.histogram(raw, stream, zeroed=consume)
-        if comm is not None:  # in-place u32 all-reduce of the 256 counts over xGMI
-            comm.allreduce_histogram(bt.hist, stream.cuda_stream)
-        bt.tables_from_hist(stream, consume=consume)
+        if fused:
+            bt.table_from_data(raw, stream)
+        else:
+            bt.histogram(raw, stream, zeroed=consume)
+            if comm is not None:  # in-place u32 all-reduce of the 256 counts over xGMI
+                comm.allreduce_histogram(bt.hist, stream.cuda_stream)
+            bt.tables_from_hist(stream, consume=consume)
         if G == 1:
             bt.encode(raw, enc, stream)
             bt.decode(enc, out, stream)

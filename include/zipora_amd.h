@@ -24,11 +24,16 @@
  * Functions with the _dev suffix take DEVICE memory, are ordered on the given
  * HIP stream (hipStream_t passed as void*, NULL = default stream) and report
  * per-buffer status into a device int32 array; read it after synchronising.
- * Graph capture: zr_rans_encode/decode_batch_dev, zr_histogram_dev and
- * zr_rans_dtab_from_hist*_dev may be captured into a HIP graph (the decoder
- * then takes its capture-safe path: no host-side call counter); the _dev calls
- * that stage host data (zr_rans_dtab_upload, zr_huff_*_dev, zr_fse_*_dev,
- * zr_ctx_huff_*_dev) return ZR_UNSUPPORTED on a capturing stream.
+ * Graph capture: zr_rans_encode/decode_batch_dev, zr_histogram_dev,
+ * zr_rans_dtab_from_hist*_dev and the RCCL calls may be captured into a HIP
+ * graph and replayed (zr_rans_decode_batch_dev then takes its capture-safe
+ * path: no host-side call counter). Every other _dev call returns
+ * ZR_UNSUPPORTED on a capturing stream: zr_rans_dtab_upload and
+ * zr_huff_decode_dev stage host data through memory a host callback frees,
+ * zr_rans_dtab_from_data_dev picks its ticket counters by a host counter, and
+ * zr_huff_encode_dev, zr_fse_compress_dev, zr_fse_decompress_dev,
+ * zr_ctx_huff_encode_dev, zr_ctx_huff_decode_dev and the
+ * zr_rans_compressor_*_batch_dev calls are not capture-validated.
  */
 #ifndef ZIPORA_AMD_H
 #define ZIPORA_AMD_H
@@ -93,8 +98,10 @@ int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches);
 /* Rans64Symbol::new(start, freq).fast_div(x) -> (x / freq, x % freq)
  * (rans.rs:89-152, the pub symbol info of Rans64Encoder::get_symbol, rans.rs:423)
  * for n dividends, computed on the device by the encoder's 24-bit reciprocal
- * division for x < 2^24 (every state the coder holds) and by 64-bit division
- * above. freq in 1..4096. Host arrays; synchronous. */
+ * division for x < 2^24 (every state the coder holds, freq <= 4096) and by
+ * 64-bit division otherwise. Any u32 freq: freq 0 gives (0, 0) as the
+ * reference's early return does (rans.rs:138-140), every other freq the exact
+ * quotient and remainder. Host arrays; synchronous. */
 int32_t zr_rans_symbol_fast_div(uint32_t start, uint32_t freq, const uint64_t *x, size_t n, uint64_t *q,
                                 uint64_t *r);
 /* Diagnostic (no reference counterpart): the number of streams / records the
@@ -148,6 +155,16 @@ int32_t zr_rans_dtab_from_hist_dev(const uint32_t *hist_dev, uint32_t n_tables, 
  * accumulating zr_histogram_dev into them needs no zr_memset_dev */
 int32_t zr_rans_dtab_from_hist_consume_dev(uint32_t *hist_dev, uint32_t n_tables, void *dtabs_dev,
                                            void *stream);
+/* the shared table of a whole batch in ONE launch: the histogram of every byte
+ * of the batch (zr_histogram_dev, shared = 1) and, in its last workgroup, the
+ * table (Rans64Encoder::new, rans.rs:208-235) into dtab_dev (one table). The
+ * RansBlobStore::train / RansCompressor::new path of a single GPU
+ * (blob_store/entropy.rs:212-222, compression/mod.rs:433-450). hist_dev: 256
+ * u32, all zero on entry, left all zero (the counts are consumed). Not on a
+ * capturing stream (ZR_UNSUPPORTED): each call picks its workgroups' ticket
+ * counters by a host-side call counter. */
+int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *batch, uint32_t *hist_dev,
+                                   void *dtab_dev, void *stream);
 /* bytes of device workspace needed by encode/decode of this batch geometry */
 size_t zr_rans_workspace_bytes(uint32_t n_buffers, uint32_t n_streams, uint64_t max_len);
 /* batched Rans64Encoder::encode: raw -> enc (enc + enc_off[b] must hold

@@ -80,3 +80,51 @@ def test_host_staging_calls_refuse_capture():
         arr = (_lib.RansTable * 1)(t)
         st = zr.load().zr_rans_dtab_upload(arr, 1, bt.tables.data_ptr(), torch.cuda.current_stream().cuda_stream)
     assert st == _lib.ZR_UNSUPPORTED
+
+
+def test_capture_refusal_list():
+    """The header's list of the _dev calls that refuse a capturing stream
+    (include/zipora_amd.h: zr_rans_dtab_upload, zr_huff_decode_dev,
+    zr_rans_dtab_from_data_dev, zr_huff_encode_dev, zr_fse_compress_dev,
+    zr_fse_decompress_dev, zr_ctx_huff_encode_dev, zr_ctx_huff_decode_dev, the
+    RansCompressor batch calls), each called under an active capture: every one
+    returns ZR_UNSUPPORTED and enqueues nothing (the captured graph is empty)."""
+    import ctypes
+    from zipora_amd import _lib
+    from zipora_amd.device import RansCompressorDeviceBatch
+    L = zr.load()
+    bt = RansDeviceBatch([5000], 4096, shared_table=True)
+    raw = bt.new_raw()
+    data = zr.synth("t", 4000, seed=3)
+    tree = zr.HuffmanEncoder(data).tree().raw
+    ctx = zr.ContextualHuffmanEncoder(data, zr.HuffmanOrder.Order1)
+    cb = RansCompressorDeviceBatch([4000])
+    buf = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    meta = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ws = torch.empty(1 << 22, dtype=torch.uint8, device="cuda")
+    cfg = _lib.FseConfig()
+    L.zr_fse_config_default(ctypes.byref(cfg))
+    side = torch.cuda.Stream()
+    got = {}
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        s = torch.cuda.current_stream().cuda_stream
+        m, st = meta.data_ptr(), meta.data_ptr() + 8
+        got["dtab_from_data"] = L.zr_rans_dtab_from_data_dev(raw.data_ptr(), bt.cbatch, bt.hist.data_ptr(),
+                                                              bt.tables.data_ptr(), s)
+        got["huff_decode"] = L.zr_huff_decode_dev(tree, buf.data_ptr(), 8192, out.data_ptr(), 4000, st,
+                                                  ws.data_ptr(), ws.numel(), s)
+        got["huff_encode"] = L.zr_huff_encode_dev(tree, buf.data_ptr(), 4000, out.data_ptr(), out.numel(), m, st,
+                                                  ws.data_ptr(), ws.numel(), s)
+        got["fse_compress"] = L.zr_fse_compress_dev(ctypes.byref(cfg), None, buf.data_ptr(), 4000, out.data_ptr(),
+                                                    m, st, ws.data_ptr(), ws.numel(), s)
+        got["fse_decompress"] = L.zr_fse_decompress_dev(buf.data_ptr(), 4000, out.data_ptr(), out.numel(), 1, m, st,
+                                                        ws.data_ptr(), ws.numel(), s)
+        got["ctx_encode"] = L.zr_ctx_huff_encode_dev(ctx.handle, 0, buf.data_ptr(), 4000, out.data_ptr(), s)
+        got["ctx_decode"] = L.zr_ctx_huff_decode_dev(ctx.handle, 0, buf.data_ptr(), 4000, out.data_ptr(), 4000, s)
+        got["compressor_compress"] = L.zr_rans_compressor_compress_batch_dev(
+            cb.cbatch, buf.data_ptr(), out.data_ptr(), cb.ws.data_ptr(), cb.ws_bytes, s)
+        got["compressor_decompress"] = L.zr_rans_compressor_decompress_batch_dev(
+            cb.cbatch, buf.data_ptr(), out.data_ptr(), cb.ws.data_ptr(), cb.ws_bytes, s)
+    assert got == {k: _lib.ZR_UNSUPPORTED for k in got}, got

@@ -55,11 +55,16 @@ def test_rans_literal_config_full_size(zr, oracle):
     assert torch.equal(out[:n], raw)
 
 
-@pytest.mark.parametrize("N,B", [(4096, 24), (1000, 70)])
-def test_rans_wide_shape_ragged(zr, oracle, N, B):
-    """More than 2^16 streams in the batch: 256-lane encoder and 1024-lane decoder
-    workgroups, with ragged, tiny (x1 layout) and empty buffers mixed in."""
+@pytest.mark.parametrize("N,B,w1024", [(4096, 24, False), (1000, 70, False), (4096, 24, True), (1024, 70, True),
+                                       (2048, 40, True), (8192, 10, True)])
+def test_rans_wide_shape_ragged(zr, oracle, N, B, w1024, monkeypatch):
+    """More than 2^16 streams in the batch: 256-lane encoder workgroups, or
+    (w1024: ZR_ENC_W=1024, N a multiple of 1024) the 1024-lane ones with 16
+    table copies, 1024-lane decoder workgroups, with ragged, tiny (x1 layout)
+    and empty buffers mixed in."""
     import torch
+    if w1024:
+        monkeypatch.setenv("ZR_ENC_W", "1024")
     from zipora_amd.device import RansDeviceBatch
     rnd = random.Random(N)
     base = [0, 1, N - 1, N, N + 1, 50000, 123457, 1 << 18, 3 * N + 7]
@@ -109,14 +114,19 @@ def test_rans_narrow_shape_ragged(zr, oracle, N):
 
 
 @pytest.mark.parametrize("N,per,B,skew", [(100, 1208, 3, False), (100, 1209, 3, False), (100, 1208, 2, True),
-                                           (4096, 1208, 17, False), (4096, 1208, 17, True), (1000, 300, 70, True)])
-def test_rans_scratch_layouts(zr, oracle, N, per, B, skew):
+                                           (4096, 1208, 17, False), (4096, 1208, 17, True), (1000, 300, 70, True),
+                                           (4096, 1209, 17, True)])
+@pytest.mark.parametrize("w1024", [False, True])
+def test_rans_scratch_layouts(zr, oracle, N, per, B, skew, w1024, monkeypatch):
     """Both scratch layouts of the xN encoder (RansWork::il): per-stream capacity
     2 * per + 16 = 2432 B is the largest lane-interleaved one, 2434 B the
     smallest stream-contiguous one. Groups of 16 streams whose destination spans
     two compaction windows, and (skew) streams of very different lengths in one
-    group: every third stream of the period-N interleave sees one constant byte."""
+    group: every third stream of the period-N interleave sees one constant byte.
+    w1024: the same with ZR_ENC_W=1024 (the 1024-lane encoder where N allows)."""
     import torch
+    if w1024:
+        monkeypatch.setenv("ZR_ENC_W", "1024")
     from zipora_amd.device import RansDeviceBatch
     lens = [N * per - (b % 3) for b in range(B)]
     datas = []
@@ -473,9 +483,9 @@ def test_shared_table_exchange_two_ranks_on_device():
 
 
 def test_wide_decode_errors_in_later_workgroups(zr, oracle):
-    """The 1024-lane decoder with its fused header (no k_dec_hdr): workgroup 0
-    of a buffer writes the first status and publishes the call's epoch, and an
-    error found by a later workgroup waits for it, so errors anywhere in a
+    """The 1024-lane decoder with its fused header (no k_dec_hdr): the last
+    workgroup of a buffer to finish stores its status from the errors every
+    workgroup added to the buffer's arrival word, so errors anywhere in a
     buffer survive. Corrupted buffers (lengths moved between two streams of the
     third workgroup, a changed state, a flipped stream bit, a truncated buffer,
     a total over enc_len) decode error-for-error and byte-for-byte like the
@@ -537,3 +547,114 @@ def test_wide_decode_errors_in_later_workgroups(zr, oracle):
         else:
             assert st[b] == 0, f"buffer {b}: the oracle decodes, GPU status {st[b]}"
             assert bt.raw_of(out, b) == ref, f"buffer {b}"
+
+
+def test_wide_decode_errors_grid_beyond_residency(zr, oracle):
+    """The decoder's status protocol without waits: every
+    workgroup of a buffer adds itself to the buffer's arrival word when its
+    lanes are done and the last one stores the status, so a grid of more
+    workgroups than the GPU holds at once (300 buffers x 4 workgroups of 1024
+    lanes, one per CU) reports errors found by the LAST workgroups of the last
+    buffers; a clean call with the same workspace then reports OK everywhere (a
+    stale arrival word of the earlier call restarts), and a corrupted call again
+    reports the errors (rans.rs:480-482, :601-610: the oracle decides)."""
+    import random
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    N, n, B = 4096, 8 * 4096, 300
+    datas = [zr.synth("u" if b % 3 else "t", n, seed=4000 + b) for b in range(B)]
+    bt = RansDeviceBatch([n] * B, N, shared_table=False)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    tabs = [oracle.rans_table(oracle.histogram(d)) for d in datas]
+    clean = bytearray(enc.cpu().numpy().tobytes())
+    clean_len = bt.enc_len.cpu().tolist()
+    host, enc_len = bytearray(clean), list(clean_len)
+    rnd = random.Random(23)
+
+    def u32(buf, o):
+        return int.from_bytes(buf[o:o + 4], "little")
+
+    bad_bufs = list(range(B - 24, B))  # the last buffers: their workgroups start last
+    for b in bad_bufs:
+        o, L = bt.enc_off_host[b], enc_len[b]
+        if b % 3 == 0:  # truncated: the last stream (workgroup 3) runs out of bytes
+            enc_len[b] = L - rnd.randrange(1, 8)
+        elif b % 3 == 1:  # 5 bytes of a stream of workgroup 3 moved to its neighbour
+            s = rnd.randrange(3072, N - 1)
+            ls, ls1 = o + 8 * N + 4 * s, o + 8 * N + 4 * (s + 1)
+            host[ls:ls + 4] = (u32(host, ls) - 5).to_bytes(4, "little")
+            host[ls1:ls1 + 4] = (u32(host, ls1) + 5).to_bytes(4, "little")
+        else:  # a state of workgroup 3 below 2^16: the generic decoder, then an error or not
+            s = rnd.randrange(3072, N)
+            host[o + 8 * s:o + 8 * s + 8] = rnd.randrange(1, 1 << 16).to_bytes(8, "little")
+
+    def run(buf, lens):
+        enc.copy_(torch.frombuffer(bytes(buf), dtype=torch.uint8).cuda())
+        bt.enc_len.copy_(torch.tensor(lens, dtype=torch.int64))
+        bt.status.fill_(-3)
+        out = bt.new_raw()
+        bt.decode(enc, out)
+        torch.cuda.synchronize()
+        return bt.statuses(), out
+
+    def check(st, out, buf, lens):
+        n_err = 0
+        for b in range(B):
+            o = bt.enc_off_host[b]
+            try:
+                ref = oracle.rans_decode(tabs[b], N, bytes(buf[o:o + lens[b]]), n)
+            except oracle.OracleError:
+                ref = None
+            if ref is None:
+                n_err += 1
+                assert st[b] != 0, f"buffer {b}: the oracle errs, the GPU reports ok"
+            else:
+                assert st[b] == 0, f"buffer {b}: the oracle decodes, GPU status {st[b]}"
+                assert bt.raw_of(out, b) == ref, f"buffer {b}"
+        return n_err
+
+    assert check(*run(host, enc_len), host, enc_len) >= 16
+    st, out = run(clean, clean_len)
+    assert all(v == 0 for v in st)
+    assert check(st, out, clean, clean_len) == 0
+    assert check(*run(host, enc_len), host, enc_len) >= 16
+
+
+@pytest.mark.parametrize("kind,B,n", [("u", 64, 4 << 20), ("t", 3, 100_000), ("z", 1, 5000), ("u", 1, 0)])
+def test_table_from_data_fused(zr, oracle, kind, B, n):
+    """zr_rans_dtab_from_data_dev (histogram + table build in the last k_hist
+    workgroup): the table equals the oracle's
+    Rans64Encoder::new of the batch's byte counts (rans.rs:208-299) and the
+    two-launch path's byte for byte, hist is left zero, the table memory may
+    hold garbage on entry, and repeated calls agree (the ticket counters are
+    left zero by each call). The batch then encodes exactly as the oracle does."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    datas = [zr.synth(kind, n, seed=77 + b) for b in range(B)]
+    bt = RansDeviceBatch([n] * B, 4096, shared_table=True)
+    raw = _fill(bt, datas)
+    ref = RansDeviceBatch([n] * B, 4096, shared_table=True)
+    ref.histogram(raw)
+    ref.tables_from_hist()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    bt.tables.copy_(torch.randint(0, 256, (bt.tables.numel(),), dtype=torch.uint8, generator=g).cuda())
+    for _ in range(3):
+        bt.table_from_data(raw)
+        torch.cuda.synchronize()
+        assert int(bt.hist.abs().sum().item()) == 0
+        w, wr = _dtab_words(bt), _dtab_words(ref)
+        assert (w[:2] == wr[:2]).all() and (w[4:] == wr[4:]).all()  # (words 2-3: padding, never written)
+    all_bytes = b"".join(datas)
+    t = oracle.rans_table(oracle.histogram(all_bytes))
+    assert list(w[4:260]) == list(t.freq) and list(w[260:516]) == list(t.start)
+    if n >= 4096:
+        enc = bt.new_enc()
+        bt.encode(raw, enc)
+        torch.cuda.synchronize()
+        bt.raise_on_error()
+        for b in range(min(B, 3)):
+            assert bt.encoded(enc, b) == oracle.rans_encode(t, 4096, datas[b])

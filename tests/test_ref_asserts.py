@@ -227,6 +227,18 @@ def test_rans_fast_div_matches_hardware_division():
     assert not bad, bad[:5]
 
 
+@gpu
+def test_rans_fast_div_zero_and_large_freq():
+    """fast_div's other inputs (rans.rs:137-152): freq 0 returns (0, 0) for every
+    x (the early return at :138-140); a freq above TOTFREQ (Rans64Symbol::new
+    takes any u32) divides exactly, as the 64-bit reciprocal does."""
+    M = (1 << 64) - 1
+    xs = [0, 1, 4095, 65536, (1 << 24) - 1, 1 << 24, M // 3, M]
+    assert zr.Rans64Symbol(0, 0).fast_div(xs) == [(0, 0)] * len(xs)
+    for f in (4097, 65537, (1 << 31) + 1, (1 << 32) - 1):
+        assert zr.Rans64Symbol(0, f).fast_div(xs) == [divmod(x, f) for x in xs], f
+
+
 # --------------------------------------------------------------------------
 # fse.rs:1464-1474 -- CPU restatement only: FseTable builds a FastDivision of
 # the frequency total (fse.rs:480) but no coding step ever calls it, so the

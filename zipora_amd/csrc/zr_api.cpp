@@ -26,15 +26,17 @@ void clear_error() { g_last_error.clear(); }
 
 // compute units of the current device (cached per device)
 uint32_t cu_count() {
-    static int cached[64] = {};
+    // (atomic slots: the thread-safe host entry points may fill them concurrently;
+    // every writer stores the same value)
+    static std::atomic<int> cached[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cached[dev]) {
-        int n = 0;
+    int n = cached[dev].load(std::memory_order_relaxed);
+    if (!n) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cached[dev] = n;
+        cached[dev].store(n, std::memory_order_relaxed);
     }
-    return (uint32_t)cached[dev];
+    return (uint32_t)n;
 }
 
 // ---------------------------------------------------------------- allocations
@@ -126,9 +128,22 @@ int32_t release_call_contexts() {
         take.swap(g_ctx_free);
     }
     int cur = 0;
-    ZR_HIP(hipGetDevice(&cur));
+    if (hipGetDevice(&cur) != hipSuccess) {  // nothing released: the contexts go back
+        std::lock_guard<std::mutex> g(g_ctx_mx);
+        for (auto &kv : take) g_ctx_free[kv.first].insert(g_ctx_free[kv.first].end(), kv.second.begin(), kv.second.end());
+        return set_error(ZR_INTERNAL, "HIP error: hipGetDevice failed");
+    }
+    // a device that cannot be selected keeps its contexts in the pool (never
+    // leaked); the other devices are still released; the first error is reported
+    int32_t st = ZR_OK;
     for (auto &kv : take) {
-        ZR_HIP(hipSetDevice(kv.first));
+        if (hipSetDevice(kv.first) != hipSuccess) {
+            std::lock_guard<std::mutex> g(g_ctx_mx);
+            auto &v = g_ctx_free[kv.first];
+            v.insert(v.end(), kv.second.begin(), kv.second.end());
+            if (st == ZR_OK) st = set_error(ZR_INTERNAL, "HIP error: hipSetDevice failed");
+            continue;
+        }
         for (CallCtx *c : kv.second) {
             for (int i = 0; i < CallCtx::NBUF; i++)
                 if (c->buf[i]) (void)hipFreeAsync(c->buf[i], c->stream);
@@ -139,8 +154,8 @@ int32_t release_call_contexts() {
         hipMemPool_t pool;
         if (hipDeviceGetDefaultMemPool(&pool, kv.first) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
     }
-    ZR_HIP(hipSetDevice(cur));
-    return ZR_OK;
+    if (hipSetDevice(cur) != hipSuccess && st == ZR_OK) st = set_error(ZR_INTERNAL, "HIP error: hipSetDevice failed");
+    return st;
 }
 
 int32_t CallLease::sync() {

@@ -224,6 +224,8 @@ int32_t zr_rans_compressor_compress_batch_dev(const zr_rans_batch *bt, const uin
                                               void *ws, size_t ws_bytes, void *stream) {
     ZR_GUARD_BEGIN
     clear_error();
+    if (capturing((hipStream_t)stream))
+        return set_error(ZR_UNSUPPORTED, "zr_rans_compressor_compress_batch_dev on a capturing stream");
     if (!bt) return set_error(ZR_INVALID_INPUT, "null batch");
     if (bt->n_streams != 1 || bt->table_stride != 0)
         return set_error(ZR_INVALID_INPUT, "RansCompressor batches are x1 with one shared table");
@@ -251,6 +253,8 @@ int32_t zr_rans_compressor_decompress_batch_dev(const zr_rans_batch *bt, const u
                                                 void *ws, size_t ws_bytes, void *stream) {
     ZR_GUARD_BEGIN
     clear_error();
+    if (capturing((hipStream_t)stream))
+        return set_error(ZR_UNSUPPORTED, "zr_rans_compressor_decompress_batch_dev on a capturing stream");
     if (!bt) return set_error(ZR_INVALID_INPUT, "null batch");
     if (bt->n_streams != 1) return set_error(ZR_INVALID_INPUT, "RansCompressor batches are x1");
     const uint32_t B = bt->n_buffers;

@@ -989,6 +989,8 @@ int32_t zr_fse_compress_dev(const zr_fse_config *c, const uint32_t *freqs_dev, c
                             void *stream) {
     ZR_GUARD_BEGIN
     clear_error();
+    if (capturing((hipStream_t)stream))
+        return set_error(ZR_UNSUPPORTED, "zr_fse_compress_dev on a capturing stream");
     int32_t st = fse_validate(c);  // FseEncoder::new (fse.rs:773-786)
     if (st) return st;
     hipStream_t s = (hipStream_t)stream;
@@ -1045,6 +1047,8 @@ int32_t zr_fse_decompress_dev(const uint8_t *in, size_t n, uint8_t *out, size_t 
                               void *stream) {
     ZR_GUARD_BEGIN
     clear_error();
+    if (capturing((hipStream_t)stream))
+        return set_error(ZR_UNSUPPORTED, "zr_fse_decompress_dev on a capturing stream");
     if (max_blocks == 0) max_blocks = 1;
     if (ws_bytes < fse_dec_ws_bytes(max_blocks)) return set_error(ZR_INVALID_INPUT, "FSE workspace too small");
     hipStream_t s = (hipStream_t)stream;

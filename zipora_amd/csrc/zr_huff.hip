@@ -748,6 +748,8 @@ int32_t zr_huff_encode_dev(const zr_huff_tree *t, const uint8_t *in, size_t n, u
                            uint64_t *out_len_dev, int32_t *status_dev, void *ws, size_t ws_bytes, void *stream) {
     ZR_GUARD_BEGIN
     clear_error();
+    if (capturing((hipStream_t)stream))
+        return set_error(ZR_UNSUPPORTED, "zr_huff_encode_dev on a capturing stream");
     hipStream_t s = (hipStream_t)stream;
     ZR_HIP(hipMemsetAsync(status_dev, 0, 4, s));
     if (n == 0) {  // encoder.rs:89-91
@@ -1029,6 +1031,8 @@ int32_t zr_ctx_huff_encode_dev(const zr_ctx_huff *h, int32_t nway, const uint8_t
                                void *stream) {
     ZR_GUARD_BEGIN
     clear_error();
+    if (capturing((hipStream_t)stream))
+        return set_error(ZR_UNSUPPORTED, "zr_ctx_huff_encode_dev on a capturing stream");
     if (h->order == 0) return set_error(ZR_UNSUPPORTED, "order-0 model: use zr_huff_encode_dev");
     if (nway != 0 && nway != 1 && nway != 2 && nway != 4 && nway != 8)
         return set_error(ZR_INVALID_INPUT, "interleaving factor must be 1, 2, 4 or 8");
@@ -1049,6 +1053,8 @@ int32_t zr_ctx_huff_decode_dev(const zr_ctx_huff *h, int32_t nway, const uint8_t
                                uint8_t *out, size_t n, void *stream) {
     ZR_GUARD_BEGIN
     clear_error();
+    if (capturing((hipStream_t)stream))
+        return set_error(ZR_UNSUPPORTED, "zr_ctx_huff_decode_dev on a capturing stream");
     if (h->order == 0) return set_error(ZR_UNSUPPORTED, "order-0 model: use zr_huff_decode_dev");
     if (nway != 0 && nway != 1 && nway != 2 && nway != 4 && nway != 8)
         return set_error(ZR_INVALID_INPUT, "interleaving factor must be 1, 2, 4 or 8");

@@ -154,9 +154,20 @@ __device__ __forceinline__ void hist_range(const uint8_t *p, uint64_t lo, uint64
 //    batch of a million 1 KiB records keeps all 64 lanes of a wave busy, and
 //    each workgroup adds one LDS histogram to the 256 global counters at the
 //    end (a global atomic per bin per record would serialise on 256 words).
+constexpr uint32_t TAB_POOL_WORDS = TOTFREQ + 3 * 256 + 16;  // tab_build's LDS scratch
+__device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_t *pool);
+__device__ __noinline__ bool tab_arrive(uint64_t epoch, uint32_t g, uint32_t nwg);
+// tab (shared mode, non-null): the fused form. Every workgroup, once its adds
+// into hist have completed, takes a ticket (tab_arrive); the last one
+// takes the complete histogram from hist (atomic exchange with 0: the counts
+// as performed at the memory side, and hist left zeroed for the next call)
+// and builds the table with its LDS (Rans64Encoder::new, rans.rs:208-235): no
+// k_tab launch and no dispatch gap between the two.
 __global__ __launch_bounds__(256) void k_hist(const uint8_t *raw, KArgs a, int shared,
-                                              uint32_t *hist, uint64_t chunk, uint32_t nchunk) {
-    __shared__ uint32_t h[256 * HCOPY];
+                                              uint32_t *hist, uint64_t chunk, uint32_t nchunk,
+                                              RansDTab *tab, uint64_t epoch) {
+    __shared__ __attribute__((aligned(16))) uint32_t h[256 * HCOPY];
+    static_assert(256 * HCOPY >= TAB_POOL_WORDS, "the table build reuses the histogram copies");
     for (int i = threadIdx.x; i < 256 * HCOPY; i += 256) h[i] = 0;
     __syncthreads();
     const uint64_t items = (uint64_t)a.B * nchunk;
@@ -183,6 +194,16 @@ __global__ __launch_bounds__(256) void k_hist(const uint8_t *raw, KArgs a, int s
     if (sum) {
         const uint32_t b = (uint32_t)(blockIdx.x / nchunk);
         atomicAdd(&hist[(shared ? 0 : (size_t)b * 256) + v], sum);
+    }
+    if (tab) {
+        __shared__ uint32_t last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adds are performed
+        __syncthreads();                                   // (and every wave's, and the copies read)
+        if (v == 0) last = tab_arrive(epoch, blockIdx.x, gridDim.x) ? 1u : 0u;
+        __syncthreads();
+        if (!last) return;
+        const uint32_t f = __hip_atomic_exchange(&hist[v], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tab_build(f, tab, h);
     }
 }
 
@@ -243,16 +264,16 @@ __global__ __launch_bounds__(256) void k_hist_small(const uint8_t *raw, KArgs a,
 // table build on device: Rans64Encoder::new (rans.rs:208-235) with
 // normalize_frequencies (rans.rs:238-299) and the symbol starts (rans.rs:225-228)
 // ======================================================================
-// clear: non-null = the histogram itself, zeroed once read (each thread its own
-// bin), so the next accumulating zr_histogram_dev needs no memset
-__global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tabs, uint32_t *clear) {
-    __shared__ unsigned long long sh[4];
-    __shared__ uint32_t norm_s[256], start_s[256], freq_raw[256];
-    __shared__ unsigned long long best;
+// One 256-thread workgroup builds table d from the raw counts, thread v
+// holding f = count of byte v. pool: LDS scratch of TAB_POOL_WORDS words,
+// 16-B aligned (k_tab's own, or k_hist's histogram copies once summed).
+__device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_t *pool) {
+    uint32_t *const mark = pool;  // TOTFREQ words (the slot owners below)
+    uint32_t *const norm_s = pool + TOTFREQ, *const start_s = norm_s + 256, *const freq_raw = start_s + 256;
+    unsigned long long *const sh = reinterpret_cast<unsigned long long *>(freq_raw + 256);  // 4
+    unsigned long long &best = sh[4];
+    uint32_t *const wmax = reinterpret_cast<uint32_t *>(sh + 5);  // 4
     const uint32_t v = threadIdx.x;
-    RansDTab *d = tabs + blockIdx.x;
-    const uint32_t f = hist[(size_t)blockIdx.x * 256 + v];
-    if (clear) clear[(size_t)blockIdx.x * 256 + v] = 0;
     freq_raw[v] = f;
     // total_freq: u32 wrapping sum (rans.rs:209)
     const uint32_t total = (uint32_t)block_sum(f, sh);
@@ -326,8 +347,6 @@ __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tab
     // 4096 slots (thread v owns slots 16v..16v+15); zero-frequency symbols
     // share the next start and are never marked, so the owner of slot j is
     // the last present symbol with start <= j
-    __shared__ __attribute__((aligned(16))) uint32_t mark[TOTFREQ];
-    __shared__ uint32_t wmax[4];
     for (uint32_t j = v; j < TOTFREQ; j += 256) mark[j] = 0;
     __syncthreads();
     if (norm > 0) mark[start] = v + 1;
@@ -366,6 +385,38 @@ __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tab
         d->kind = maxn ? DT_SINGLE : DT_NORMAL;
         d->status = ZR_OK;
     }
+}
+
+// clear: non-null = the histogram itself, zeroed once read (each thread its own
+// bin), so the next accumulating zr_histogram_dev needs no memset
+__global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tabs, uint32_t *clear) {
+    __shared__ __attribute__((aligned(16))) uint32_t pool[TAB_POOL_WORDS];
+    const uint32_t v = threadIdx.x;
+    const uint32_t f = hist[(size_t)blockIdx.x * 256 + v];
+    if (clear) clear[(size_t)blockIdx.x * 256 + v] = 0;
+    tab_build(f, tabs + blockIdx.x, pool);
+}
+
+// The workgroups of k_hist's fused form (shared histogram, then the table):
+// each, once its histogram adds have completed, takes a ticket. Tickets are
+// sharded: workgroup g adds to counter g % 8 of the call's slot, the last of
+// each shard adds to the slot's top counter, and the last there builds the
+// table (returns true). Plain returning atomic adds (a CAS per workgroup on
+// one word took 2.9 ms at 1280 workgroups: every contender a memory round
+// trip); one word takes ~88 adds per us, so 8 shards of <= 160. The counters
+// are library memory, zero at load, and every counter is reset to zero by its
+// last adder, so no call needs a memset; a call uses slot epoch % TT_SLOTS
+// (calls in flight at once on other streams: fewer than TT_SLOTS).
+constexpr uint32_t TT_SLOTS = 64;
+__device__ unsigned int g_tab_tick[TT_SLOTS][9];
+__device__ __noinline__ bool tab_arrive(uint64_t epoch, uint32_t g, uint32_t nwg) {
+    unsigned int *const t = g_tab_tick[epoch % TT_SLOTS];
+    const uint32_t sh = g & 7, in_sh = (nwg - sh + 7) / 8, nsh = min(nwg, 8u);
+    if (__hip_atomic_fetch_add(&t[sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 != in_sh) return false;
+    __hip_atomic_store(&t[sh], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(&t[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 != nsh) return false;
+    __hip_atomic_store(&t[8], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
 }
 
 __device__ __forceinline__ void asm_load16(v4u &dst, uintptr_t addr) {
@@ -419,6 +470,17 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 #ifndef ZR_ENC_DB
 #define ZR_ENC_DB 1
 #endif
+#ifndef ZR_ENC_1024
+#define ZR_ENC_1024 0  // the 1024-lane encoder by default (else only with ZR_ENC_W=1024)
+#endif
+static bool enc_w1024() {
+    if (ZR_ENC_1024) return true;
+    const char *e = getenv("ZR_ENC_W");
+    return e && atoi(e) == 1024;
+}
+#ifndef ZR_ENC_PF
+#define ZR_ENC_PF 1
+#endif
 template <uint32_t EW, int ABL, bool IL>
 __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
     // DB: two input tiles, written alternately, so one barrier per tile
@@ -430,10 +492,23 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     constexpr uint32_t FL = ERS / 2;        // dwords per flush burst
     constexpr uint32_t ETILE = 16;          // input rows (steps) per tile
     constexpr uint32_t RING_BYTES = ERS * EW * 4;  // a power of two
-    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16 + (DB ? 2 : 1) * ETILE * EW];
+    // TC: copies of the encode table. The 1024-lane shape (one workgroup per
+    // CU) keeps 16: entry v's copies side by side ((v * 16 + c) * 16 B), lane l
+    // reading copy l & 15, so the 16 lanes of each ds_read_b128 lane group
+    // ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and +32) read 16 different bank
+    // quads: no bank conflicts, whatever the symbols (one copy: 16 random
+    // entries over 16 quads, ~7.7 extra LDS cycles per wave-step). 64 KiB ring +
+    // 64 KiB table + 32 KiB tiles = the CU's 160 KiB.
+    constexpr uint32_t TC = EW == 1024 ? 16 : 1;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16 * TC + (DB ? 2 : 1) * ETILE * EW];
     uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
     uint4 *et = reinterpret_cast<uint4 *>(lds + RING_BYTES);
-    uint8_t *itile = lds + RING_BYTES + 256 * 16;
+    uint8_t *itile = lds + RING_BYTES + 256 * 16 * TC;
+    // this lane's copy, as the byte offset of entry 0 (entry v: + v * 16 * TC)
+    const uint32_t et_lane = (threadIdx.x & (TC - 1)) * 16;
+    auto ent = [&](uint32_t sym) -> const uint4 & {
+        return *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(et) + sym * (16 * TC) + et_lane);
+    };
     const uint32_t nblkE = (a.N + EW - 1) / EW;
     // one-wave workgroups: the two 64-column halves of each 128-B input line go
     // to workgroups on the same XCD (workgroups are dealt to the 8 XCDs round
@@ -458,10 +533,11 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // 0xFFFF = never, freq >= 16); y = start << 8; z = reciprocal;
     // w = (4096 - freq) << 8 | rsh << 24 (mad_u24 reads the low 24 bits)
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
-    for (uint32_t v = tid; v < 256; v += EW) {
+    for (uint32_t i = tid; i < 256 * TC; i += EW) {
+        const uint32_t v = i / TC;
         const uint32_t f = T->freq[v];
         const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
-        et[v] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
+        et[i] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
                            (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
     }
     // Input rows k*N + EW*blk .. +EW-1 are staged through the LDS tile of ETILE
@@ -536,12 +612,26 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     constexpr uint32_t ROW = EW * 4;  // ring row bytes
     uint32_t ra = tid * 4;            // + ROW * nw (mod 2^32: a multiple of RING_BYTES)
     uint32_t nw32 = 0;                // 32 * dwords completed
+    // W16 (a 64 KiB ring: the 1024-lane shape): ra kept mod 2^16 by 16-bit
+    // arithmetic (one v_mad_u16 per pair, no wrap AND), and nw not counted per
+    // pair: the pending dwords are the ring rows between ra and the flushed row
+    constexpr bool W16 = RING_BYTES == 65536;
+    uint32_t ra16 = tid * 4;  // (W16: only ever written by 16-bit ops, so < 2^16)
     uint32_t nfl = 0;                 // dwords moved to scratch
     // two steps' bits (A first) -> acc, then the ring
     auto push2 = [&](uint32_t bA, uint32_t nbA, uint32_t bB, uint32_t nbB) {
         const uint32_t cpair = bA | (bB << nbA);  // <= 32 bits
         acc |= (uint64_t)cpair << nacc;
         nacc += nbA + nbB;  // < 64
+        if constexpr (W16) {
+            *reinterpret_cast<uint32_t *>(lds + ra16) = (uint32_t)acc;
+            const uint32_t t32 = nacc & 32;
+            // ra16 = (t32 * ROW / 32 + ra16) mod 2^16: the ring wraps by itself
+            asm("v_mad_u16 %0, %1, %2, %0" : "+v"(ra16) : "v"(t32), "s"(ROW / 32));
+            acc >>= t32;
+            nacc &= 31;
+            return;
+        }
         *reinterpret_cast<uint32_t *>(lds + (ra & (RING_BYTES - 1))) = (uint32_t)acc;
         const uint32_t t32 = nacc & 32;
         ra += t32 * (ROW / 32);
@@ -549,7 +639,12 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         acc >>= t32;
         nacc &= 31;
     };
-    auto nw_of = [&]() -> uint32_t { return nw32 >> 5; };
+    // dwords completed: counted (nw32), or (W16) the flushed ones plus the ring
+    // rows from the flushed row to ra's (fewer than ERS are ever pending)
+    auto nw_of = [&]() -> uint32_t {
+        if constexpr (W16) return nfl + ((ra16 / ROW - nfl) & (ERS - 1));
+        return nw32 >> 5;
+    };
     auto flush64 = [&]() {  // tile boundary: at most one 64-B burst per lane
         const bool need = nw_of() - nfl >= FL;
         {
@@ -586,8 +681,40 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         const uint4 v = load_piece(t);
         return v4u{v.x, v.y, v.z, v.w};
     };
-    // one full tile, rows ETILE-1 .. 0, every lane a stream with all rows valid
+    // one full tile, rows ETILE-1 .. 0, every lane a stream with all rows valid.
+    // PF: the tile's 16 symbols are read first and each group's four table
+    // entries one group ahead, so the two dependent LDS round trips (symbol,
+    // then entry) of a group overlap the previous group's coding
+    auto tile_fast_pf = [&](const uint8_t *tl) {
+        uint32_t sy[ETILE];
+#pragma unroll
+        for (int r = 0; r < (int)ETILE; r++) sy[r] = tl[r * EW + tid];
+        uint4 c3 = ent(sy[ETILE - 1]), c2 = ent(sy[ETILE - 2]), c1 = ent(sy[ETILE - 3]), c0 = ent(sy[ETILE - 4]);
+#pragma unroll
+        for (int g = ETILE - 4; g >= 0; g -= 4) {
+            uint4 n3 = c3, n2 = c2, n1 = c1, n0 = c0;
+            if (g >= 4) {
+                n3 = ent(sy[g - 1]);
+                n2 = ent(sy[g - 2]);
+                n1 = ent(sy[g - 3]);
+                n0 = ent(sy[g - 4]);
+            }
+            xmin = min(xmin, min(min(c3.x, c2.x), min(c1.x, c0.x)));
+            uint32_t m3, m2, m1, m0;
+            const uint32_t b3 = enc(c3, true, m3);
+            const uint32_t b2 = enc(c2, true, m2);
+            push2(b3, m3, b2, m2);
+            const uint32_t b1 = enc(c1, true, m1);
+            const uint32_t b0 = enc(c0, true, m0);
+            push2(b1, m1, b0, m0);
+            c3 = n3, c2 = n2, c1 = n1, c0 = n0;
+        }
+    };
     auto tile_fast = [&](const uint8_t *tl) {
+        if constexpr (ZR_ENC_PF != 0 && EW == 1024 && !(ABL & 2)) {  // (256 lanes: measured no gain)
+            tile_fast_pf(tl);
+            return;
+        }
 #pragma unroll
         for (int g = ETILE - 4; g >= 0; g -= 4) {
             uint32_t s3 = tl[(g + 3) * EW + tid], s2 = tl[(g + 2) * EW + tid];
@@ -596,7 +723,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
                 const uint32_t t = (tid + (s0 & 1)) & 255;
                 s3 = s2 = s1 = s0 = t;
             }
-            const uint4 e3 = et[s3], e2 = et[s2], e1 = et[s1], e0 = et[s0];
+            const uint4 e3 = ent(s3), e2 = ent(s2), e1 = ent(s1), e0 = ent(s0);
             xmin = min(xmin, min(min(e3.x, e2.x), min(e1.x, e0.x)));
             uint32_t n3, n2, n1, n0;
             const uint32_t b3 = enc(e3, true, n3);
@@ -647,7 +774,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
             for (uint32_t r = rtop; r-- > 0;) {
                 const uint64_t k = t * ETILE + r;
                 const uint32_t sym = tl[r * EW + tid];
-                const uint4 e = et[sym];
+                const uint4 e = ent(sym);
                 const bool valid = active && k < c;
                 err |= valid && e.x == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
                 uint32_t nb;
@@ -677,20 +804,29 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         w.st_state[(size_t)b * N + s] = X >> 8;
         w.st_len[(size_t)b * N + s] = bytes;
     }
-    // byte sum of the 256-stream block (the unit of the offset scan); the
+    // byte sum of each 256-stream block (the unit of the offset scan); the
     // scan scratch aliases the input tile, free once every wave is past it
-    if (EW == 256) {
+    if (EW >= 256) {
         __syncthreads();
-        // one reduction (no extra LDS: the workgroup's 40 KiB are exact for four
-        // per CU): bytes (< 2^40) and, from bit 55, the count of lanes in error
+        // one reduction per block of 256 lanes (4 waves): bytes (< 2^40) and,
+        // from bit 55, the count of lanes in error
         unsigned long long *sh = reinterpret_cast<unsigned long long *>(itile);
-        uint64_t r;
-        const uint64_t ex = block_excl_scan((active ? bytes : 0) | ((uint64_t)bad << 55), sh, &r);
+        const uint64_t v = (active ? bytes : 0) | ((uint64_t)bad << 55);
+        const unsigned long long inc = wave_incl_scan(v);
+        const uint32_t wv = tid >> 6, w0 = wv & ~3u;  // this wave, its block's first
+        if ((tid & 63) == 63) sh[wv] = inc;
+        __syncthreads();
+        uint64_t base = 0;
+        for (uint32_t i = w0; i < wv; i++) base += sh[i];
+        const uint64_t r = sh[w0] + sh[w0 + 1] + sh[w0 + 2] + sh[w0 + 3];
+        const uint64_t ex = base + inc - v;
         // the stream's offset in the block: the compaction reads its 16 streams'
         // offsets instead of scanning the block again (a block's bytes < 2^32:
         // the compaction uses this only for buffers below 4 GiB)
         if (active) w.st_off[(size_t)b * N + s] = (uint32_t)(ex & ((1ull << 55) - 1));
-        if (tid == 0) w.blocksum[(size_t)b * w.nblk + blk] = (r & ((1ull << 55) - 1)) | ((r >> 55) ? BS_ERR : 0);
+        const uint32_t blk256 = (blk * EW + tid) / 256;
+        if ((tid & 255) == 0 && blk256 < w.nblk)
+            w.blocksum[(size_t)b * w.nblk + blk256] = (r & ((1ull << 55) - 1)) | ((r >> 55) ? BS_ERR : 0);
     } else {  // narrow workgroups add their wave sums into the zeroed block sum
         const uint64_t ws = wave_sum(active ? bytes : 0);
         const bool wbad = __any(bad);
@@ -1241,16 +1377,54 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
 // records written to the workspace scratch area; wide shape only: 64 refills
 // land without their LDS writes, 128 refill loads read a table line instead of
 // the stream, 256 every store of a wave goes to the same 256 B, 512 no wait for
-// the refill loads at the boundaries); the product instantiates ABL = 0.
+// the refill loads at the boundaries, 1024 no tile boundaries at all: no refill
+// loads, waits, landings or ring checks, i.e. the minimal instruction stream of
+// the chain, the ring reads and the packed stores); the product instantiates ABL = 0.
 //
 // epoch (non-zero): this kernel also does k_dec_hdr's work (nblk <= SCAN_FUSE):
 // every workgroup reads all N stream lengths of its buffer for its own offset
-// and the buffer's checks, workgroup 0 of the buffer writes the call's first
-// status and then publishes `epoch` (unique per call) in the buffer's flag word
-// (blockoff[b * nblk], unused at this nblk); a workgroup that finds an error
-// waits for that flag before it stores ZR_INVALID_INPUT, so no OK overwrites
-// an error (the wait never spins in practice: workgroup 0 writes at its start,
-// errors come at the end). epoch == 0: k_dec_hdr (and k_scan) ran first.
+// and the buffer's checks. The buffer's status is then written once, by the
+// last of its workgroups to finish: each workgroup, when all its lanes are
+// done, adds itself to the buffer's arrival word (blockoff[b * nblk], unused
+// at this nblk) = epoch tag << 24 | error << 23 | arrivals, by one CAS that
+// restarts the count when the word holds another call's tag; the workgroup
+// whose add completes the count stores OK or ZR_INVALID_INPUT. No workgroup
+// ever waits for another, so nothing depends on dispatch order or residency.
+// epoch == 0: k_dec_hdr (and k_scan) ran first and wrote the first status;
+// a lane in error then stores ZR_INVALID_INPUT itself.
+// A workgroup of buffer b is done (epoch mode of k_dec_xn_fast): it adds
+// itself to an arrival word = tag << 24 | error << 23 | arrivals by one CAS
+// that restarts the count when the word holds another call's tag. Lock-free:
+// a failed CAS means another workgroup's add landed. A CAS is one memory
+// round trip and k contenders on one word take k of them, so a buffer of more
+// than DA_SET workgroups (the one-wave shape: 64 per 4096 streams) arrives in
+// two levels: sets of DA_SET workgroups on words wbase[1 + set], and the last
+// of each set on wbase[0] (at most a few contenders per word). The arrival
+// that completes the buffer stores its status. wbase: blockoff[b * nblk ..],
+// 1 + ceil(nwg / DA_SET) <= nblk words when nwg > DA_SET.
+constexpr uint32_t DA_SET = 8;
+__device__ __forceinline__ bool arrive_word(uint64_t *word, uint64_t tag, bool &err, uint32_t n) {
+    uint64_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t nw;
+    do {
+        nw = ((old >> 24) == tag ? old + 1 : (tag << 24) | 1) | ((uint64_t)err << 23);
+    } while (!__hip_atomic_compare_exchange_weak(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
+    err = (nw >> 23) & 1;  // the errors of every arrival so far
+    return (nw & 0x7FFFFF) == n;
+}
+__device__ __noinline__ void dec_arrive(uint64_t *wbase, uint64_t epoch, bool err, uint32_t blkF, uint32_t nwg,
+                                        int32_t *status) {
+    const uint64_t tag = epoch & ((1ull << 40) - 1);
+    if (nwg > DA_SET) {
+        const uint32_t set = blkF / DA_SET;
+        const uint32_t in_set = min(DA_SET, nwg - set * DA_SET);
+        if (!arrive_word(wbase + 1 + set, tag, err, in_set)) return;
+        nwg = (nwg + DA_SET - 1) / DA_SET;  // the sets arrive on wbase[0]
+    }
+    if (arrive_word(wbase, tag, err, nwg)) *status = err ? ZR_INVALID_INPUT : ZR_OK;
+}
+
 template <int FW, int ABL, bool WT = false>
 __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
                                                uint32_t nblkF, uint64_t epoch) {
@@ -1349,11 +1523,10 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             __syncthreads();
         }
         const bool ok = hdr_ok && (uint64_t)N * 12 + tot <= a.enc_len[b];
-        if (blkF == 0 && tid == 0) {  // the call's first status write for this buffer
-            a.status[b] = ok ? ZR_OK : ZR_INVALID_INPUT;
-            __hip_atomic_store(eflag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (!ok) {  // (workgroup-uniform: every workgroup of the buffer sees it)
+            if (tid == 0) dec_arrive(eflag, epoch, true, blkF, nblkF, a.status + b);
+            return;
         }
-        if (!ok) return;  // (workgroup-uniform)
         blo = lo;
     } else {
         // the scan of k_dec_hdr's block sums (fused for nblk <= SCAN_FUSE: every
@@ -1371,13 +1544,29 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             blo = w.blockoff[(size_t)b * nblk + blk0];
         }
     }
-    // an error of this workgroup: ZR_INVALID_INPUT once the call's first status
-    // write is visible (epoch mode)
+    // an error of this lane: stored at once (epoch == 0), or carried to the
+    // workgroup's arrival (epoch mode, `finish` below)
+    bool lane_err = false;
     auto set_invalid = [&]() {
         if (epoch)
-            while (__hip_atomic_load(eflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)
-                __builtin_amdgcn_s_sleep(8);
-        a.status[b] = ZR_INVALID_INPUT;
+            lane_err = true;
+        else
+            a.status[b] = ZR_INVALID_INPUT;
+    };
+    // epoch mode: every wave of the workgroup ends here; once all are done, the
+    // workgroup's errors are OR-ed (one word per wave in the ring, free by then)
+    // and thread 0 arrives for the workgroup
+    auto finish = [&]() {
+        if (!epoch) return;
+        __syncthreads();
+        const bool we = __any(lane_err);
+        if ((tid & 63) == 0) ring[tid >> 6] = we ? 1u : 0u;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t e = 0;
+            for (uint32_t i = 0; i < FW / 64; i++) e |= ring[i];
+            dec_arrive(eflag, epoch, e != 0, blkF, nblkF, a.status + b);
+        }
     };
     {  // the slot table into LDS (before the barrier below)
         v4u *dst = reinterpret_cast<v4u *>(lds);
@@ -1433,6 +1622,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     };
     if (any_slow) {
         if (active) generic();
+        finish();
         return;
     }
     const uintptr_t pend = sb + L;
@@ -1563,7 +1753,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3, bool &pmine, bool pother) __attribute__((always_inline)) {
         // every read of the previous tile was at or above pos - 4 (the no-refill
         // ablation reads stale ring bytes on purpose: no fallback there)
-        bad |= !(ABL & (4 | 64 | 128)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if (t >= 2) {
             // wait for the loads of boundary t-2: younger are the 16 stores of tile
             // t-2, the 4 loads of boundary t-1 and the 16 stores of tile t-1 (every
@@ -1671,7 +1861,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     constexpr bool PAIR = ZR_DEC_PAIR && !PF;
     bool hasB = false;  // PAIR: o holds the segment below e's, loaded, not yet landed
     auto boundary_w = [&](uint32_t t, bool pk) __attribute__((always_inline)) {
-        bad |= !(ABL & (4 | 64 | 128)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if (t >= 1) {
             // the loads of boundary t - 1; younger: tile t-1's stores
             if (ABL & 512)
@@ -1736,7 +1926,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
                             (uint32_t)(wave_all && (N & 3) == 0 && ((((uintptr_t)outb) & 3) == 0))) != 0;
         if (pk) {
             for (uint32_t t = 0; t < nfull; t++) {
-                boundary_w(t, true);
+                if (!(ABL & 1024)) boundary_w(t, true);
                 tile_w(t, true);
             }
         } else {
@@ -1760,7 +1950,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         // ---- last tile (1..DT2 steps): every segment in flight lands first
         asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
                      "+v"(o2), "+v"(o3)::"memory");
-        bad |= !(ABL & (4 | 64 | 128)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+        bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
         if constexpr (PF) {
             if (pnd_o) land(o0, o1, o2, o3);
             if (pnd_e) land(e0, e1, e2, e3);
@@ -1776,7 +1966,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         for (uint32_t j = 0; j < nst; j++) {
             const uint64_t k = k0 + j;
             const bool live = k < c;
-            if (live) bad |= !(ABL & (4 | 64 | 128)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+            if (live) bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
             uint32_t h, l, sf;
             const uint32_t ent = step(readD(pos8), h, l, sf);
             pos8 = pos8 + 8 - sf;
@@ -1803,6 +1993,7 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
             }
         }
     }
+    finish();
 }
 
 __global__ __launch_bounds__(64) void k_dec_x1_generic(const uint8_t *enc, uint8_t *raw, KArgs a) {
@@ -2632,14 +2823,21 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
 // ======================================================================
 // Rans64Symbol::new(start, freq).fast_div(x) (rans.rs:89-152) on the device: the
 // encoder's own 24-bit reciprocal division (enc_div, every x < 2^24 the coder
-// can hold), the 64-bit quotient beyond that domain
+// can hold, freq <= 4096), the 64-bit quotient beyond that domain (any u32
+// freq: the reference's reciprocal is exact for every u64 x); freq == 0 gives
+// (0, 0) as the reference's early return does (rans.rs:138-140)
 __global__ __launch_bounds__(256) void k_fast_div(uint32_t freq, const uint64_t *x, uint64_t n, uint64_t *q,
                                                   uint64_t *r) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint64_t v = x[i];
+    if (freq == 0) {
+        q[i] = 0;
+        r[i] = 0;
+        return;
+    }
     uint64_t qq;
-    if (v < (1ull << 24))
+    if (v < (1ull << 24) && freq <= TOTFREQ)
         qq = enc_div((uint32_t)v, enc_rcp(freq), enc_rsh(freq));
     else
         qq = v / freq;
@@ -2738,9 +2936,10 @@ int32_t rans_carve(uint32_t B, uint32_t N, uint64_t max_len, void *ws, size_t by
 // a per-call tag, never 0, never repeated in the process (k_dec_xn_fast's
 // first-status flag: a flag word left by an earlier call holds an older value)
 static uint64_t next_epoch() {
+    // (k_dec_xn_fast tags its arrival words with the low 40 bits: never 0)
     static std::atomic<uint64_t> ctr{0x9E3779B97F4A7C15ull};
     uint64_t v;
-    do v = ctr.fetch_add(1, std::memory_order_relaxed) + 1; while (v == 0);
+    do v = ctr.fetch_add(1, std::memory_order_relaxed) + 1; while ((v & ((1ull << 40) - 1)) == 0);
     return v;
 }
 
@@ -2814,7 +3013,6 @@ int32_t zr_rans_symbol_fast_div(uint32_t start, uint32_t freq, const uint64_t *x
     clear_error();
     (void)start;  // Rans64Symbol::fast_div reads only the frequency
     if (n && (!x || !q || !r)) return set_error(ZR_INVALID_INPUT, "null argument");
-    if (freq == 0 || freq > TOTFREQ) return set_error(ZR_INVALID_INPUT, "frequency outside 1..4096");
     if (n == 0) return ZR_OK;
     if (n > (1u << 24)) return set_error(ZR_UNSUPPORTED, "more than 2^24 dividends per call");
     CallLease L;
@@ -2855,8 +3053,27 @@ int32_t zr_histogram_dev(const uint8_t *raw, const zr_rans_batch *bt, int32_t sh
                      hist_dev);
     } else {
         launch_timed("histogram", k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a,
-                     shared, hist_dev, chunk, nchunk);
+                     shared, hist_dev, chunk, nchunk, (RansDTab *)nullptr, (uint64_t)0);
     }
+    ZR_HIP(hipGetLastError());
+    return ZR_OK;
+    ZR_GUARD_END
+}
+
+int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *bt, uint32_t *hist_dev, void *dtab_dev,
+                                   void *stream) {
+    ZR_GUARD_BEGIN
+    clear_error();
+    if (!bt || !hist_dev || !dtab_dev) return set_error(ZR_INVALID_INPUT, "null argument");
+    if (capturing((hipStream_t)stream))  // the per-call tag comes from a host counter
+        return set_error(ZR_UNSUPPORTED, "zr_rans_dtab_from_data_dev on a capturing stream");
+    KArgs a = kargs(bt);
+    const uint64_t chunk = 64 * 1024;
+    const uint32_t nchunk = bt->max_len ? (uint32_t)ceil_div(bt->max_len, chunk) : 1u;
+    const uint64_t items = (uint64_t)nchunk * a.B;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(items, 4), 1280));
+    launch_timed("histogram", k_hist, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, raw, a, 1, hist_dev,
+                 chunk, nchunk, reinterpret_cast<RansDTab *>(dtab_dev), next_epoch());
     ZR_HIP(hipGetLastError());
     return ZR_OK;
     ZR_GUARD_END
@@ -2917,9 +3134,18 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
 #else
         auto kenc = w.il ? k_enc_xn<256, 0, true> : k_enc_xn<256, 0, false>;
 #endif
+        // the 1024-lane shape (16 conflict-free table copies, one workgroup per
+        // CU) where whole workgroups of streams fill the buffers: measured in
+        // round 4 at -3 % encoder time but +13 % in the
+        // compaction that follows, so the 256-lane shape stays the default and
+        // ZR_ENC_W=1024 selects the other (tests and A/B runs)
+        const bool wide = enc_w1024() && !narrow && a.N % 1024 == 0;
         if (narrow)
             launch_timed("rans_encode", w.il ? k_enc_xn<64, 0, true> : k_enc_xn<64, 0, false>,
                          dim3((uint32_t)round_up(ceil_div(a.N, 64) * a.B, 16)), dim3(64), 0, s, raw, a, w);
+        else if (wide)
+            launch_timed("rans_encode", w.il ? k_enc_xn<1024, 0, true> : k_enc_xn<1024, 0, false>,
+                         dim3((uint32_t)(a.N / 1024 * a.B)), dim3(1024), 0, s, raw, a, w);
         else
             launch_timed("rans_encode", kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
         {
@@ -3037,6 +3263,8 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
                 case 256: kern = k_dec_xn_fast<1024, 256, ZR_DEC_T8 != 0>; break;
                 case 512: kern = k_dec_xn_fast<1024, 512, ZR_DEC_T8 != 0>; break;
                 case 576: kern = k_dec_xn_fast<1024, 576, ZR_DEC_T8 != 0>; break;
+                case 1024: kern = k_dec_xn_fast<1024, 1024, ZR_DEC_T8 != 0>; break;
+                case 1025: kern = k_dec_xn_fast<1024, 1025, ZR_DEC_T8 != 0>; break;
                 default: break;
             }
 #else

@@ -92,6 +92,15 @@ class RansDeviceBatch:
         fn = self.L.zr_rans_dtab_from_hist_consume_dev if consume else self.L.zr_rans_dtab_from_hist_dev
         check(fn(_ptr(self.hist), self.n_tables, _ptr(self.tables), _stream(stream)))
 
+    def table_from_data(self, raw, stream=None):
+        """Shared table of the whole batch in one launch (histogram + the table
+        build in its last workgroup). self.hist must be all zero (fresh, or left
+        so by this call or tables_from_hist(consume=True)); it stays zero."""
+        if not self.shared:
+            raise ValueError("table_from_data builds the one shared table")
+        check(self.L.zr_rans_dtab_from_data_dev(_ptr(raw), ctypes.byref(self.cbatch), _ptr(self.hist),
+                                                _ptr(self.tables), _stream(stream)))
+
     def upload_tables(self, host_tables):
         arr = (_lib.RansTable * len(host_tables))(*host_tables)
         check(self.L.zr_rans_dtab_upload(arr, len(host_tables), _ptr(self.tables), _stream()))
