@@ -165,6 +165,11 @@ int32_t zr_rans_dtab_from_hist_consume_dev(uint32_t *hist_dev, uint32_t n_tables
  * counters by a host-side call counter. */
 int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *batch, uint32_t *hist_dev,
                                    void *dtab_dev, void *stream);
+/* Tuning (no reference counterpart): the workgroup width of the xN encoder for
+ * batches of more than 2^16 streams, process-wide: 256 (default) or 1024 (one
+ * workgroup per CU with 16 conflict-free copies of the encode table; used
+ * where n_streams % 1024 == 0). Output bytes are identical either way. */
+int32_t zr_rans_set_encoder_width(uint32_t lanes);
 /* bytes of device workspace needed by encode/decode of this batch geometry */
 size_t zr_rans_workspace_bytes(uint32_t n_buffers, uint32_t n_streams, uint64_t max_len);
 /* batched Rans64Encoder::encode: raw -> enc (enc + enc_off[b] must hold

@@ -17,6 +17,18 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+@pytest.fixture
+def enc_width(zr):
+    """Sets the xN encoder's workgroup width for one test, 256 again after it."""
+    L = zr.load()
+
+    def set_w(n):
+        assert L.zr_rans_set_encoder_width(n) == 0
+
+    yield set_w
+    L.zr_rans_set_encoder_width(256)
+
+
 def _fill(bt, datas):
     import torch
     raw = bt.new_raw()
@@ -57,14 +69,13 @@ def test_rans_literal_config_full_size(zr, oracle):
 
 @pytest.mark.parametrize("N,B,w1024", [(4096, 24, False), (1000, 70, False), (4096, 24, True), (1024, 70, True),
                                        (2048, 40, True), (8192, 10, True)])
-def test_rans_wide_shape_ragged(zr, oracle, N, B, w1024, monkeypatch):
+def test_rans_wide_shape_ragged(zr, oracle, N, B, w1024, enc_width):
     """More than 2^16 streams in the batch: 256-lane encoder workgroups, or
-    (w1024: ZR_ENC_W=1024, N a multiple of 1024) the 1024-lane ones with 16
-    table copies, 1024-lane decoder workgroups, with ragged, tiny (x1 layout)
-    and empty buffers mixed in."""
+    (w1024: zr_rans_set_encoder_width(1024), N a multiple of 1024) the 1024-lane
+    ones with 16 table copies, 1024-lane decoder workgroups, with ragged, tiny
+    (x1 layout) and empty buffers mixed in."""
     import torch
-    if w1024:
-        monkeypatch.setenv("ZR_ENC_W", "1024")
+    enc_width(1024 if w1024 else 256)
     from zipora_amd.device import RansDeviceBatch
     rnd = random.Random(N)
     base = [0, 1, N - 1, N, N + 1, 50000, 123457, 1 << 18, 3 * N + 7]
@@ -117,16 +128,15 @@ def test_rans_narrow_shape_ragged(zr, oracle, N):
                                            (4096, 1208, 17, False), (4096, 1208, 17, True), (1000, 300, 70, True),
                                            (4096, 1209, 17, True)])
 @pytest.mark.parametrize("w1024", [False, True])
-def test_rans_scratch_layouts(zr, oracle, N, per, B, skew, w1024, monkeypatch):
+def test_rans_scratch_layouts(zr, oracle, N, per, B, skew, w1024, enc_width):
     """Both scratch layouts of the xN encoder (RansWork::il): per-stream capacity
     2 * per + 16 = 2432 B is the largest lane-interleaved one, 2434 B the
     smallest stream-contiguous one. Groups of 16 streams whose destination spans
     two compaction windows, and (skew) streams of very different lengths in one
     group: every third stream of the period-N interleave sees one constant byte.
-    w1024: the same with ZR_ENC_W=1024 (the 1024-lane encoder where N allows)."""
+    w1024: the same with the 1024-lane encoder where N allows."""
     import torch
-    if w1024:
-        monkeypatch.setenv("ZR_ENC_W", "1024")
+    enc_width(1024 if w1024 else 256)
     from zipora_amd.device import RansDeviceBatch
     lens = [N * per - (b % 3) for b in range(B)]
     datas = []

@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(_PKG, "libzipora_amd.so")
 # read ZR_ABLATE / ZR_DEC_ABL / ZR_COMPACT_OLD), ZR_LIB_PATH another build (A/B
 # runs); bench.py refuses to print a metric line under either
 DIAG_LIB_PATH = os.path.join(_PKG, "libzipora_amd_diag.so")
-DIAG_ENV = ("ZR_CMP_ABL", "ZR_DIAG_LIB", "ZR_LIB_PATH", "ZR_ABLATE", "ZR_DEC_ABL", "ZR_COMPACT_OLD", "ZR_ENC_W")
+DIAG_ENV = ("ZR_CMP_ABL", "ZR_DIAG_LIB", "ZR_LIB_PATH", "ZR_ABLATE", "ZR_DEC_ABL", "ZR_COMPACT_OLD")
 
 
 def diag_env():
@@ -90,6 +90,7 @@ SIGNATURES = [
     ("zr_rans_dtab_from_hist_dev", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp]),
     ("zr_rans_dtab_from_hist_consume_dev", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp]),
     ("zr_rans_dtab_from_data_dev", ctypes.c_int32, [c_vp, ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp]),
+    ("zr_rans_set_encoder_width", ctypes.c_int32, [ctypes.c_uint32]),
     ("zr_rans_workspace_bytes", c_sz, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     ("zr_rans_encode_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp, c_sz,
                                                   c_vp]),

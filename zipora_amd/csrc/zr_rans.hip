@@ -470,14 +470,10 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 #ifndef ZR_ENC_DB
 #define ZR_ENC_DB 1
 #endif
-#ifndef ZR_ENC_1024
-#define ZR_ENC_1024 0  // the 1024-lane encoder by default (else only with ZR_ENC_W=1024)
-#endif
-static bool enc_w1024() {
-    if (ZR_ENC_1024) return true;
-    const char *e = getenv("ZR_ENC_W");
-    return e && atoi(e) == 1024;
-}
+// the xN encoder's workgroup width for batches of more than 2^16 streams
+// (zr_rans_set_encoder_width: 256, the default, or 1024 where N % 1024 == 0)
+static std::atomic<uint32_t> g_enc_width{256};
+static bool enc_w1024() { return g_enc_width.load(std::memory_order_relaxed) == 1024; }
 #ifndef ZR_ENC_PF
 #define ZR_ENC_PF 1
 #endif
@@ -2969,6 +2965,13 @@ extern "C" {
 
 size_t zr_rans_dtab_bytes(void) { return sizeof(RansDTab); }
 
+int32_t zr_rans_set_encoder_width(uint32_t lanes) {
+    clear_error();
+    if (lanes != 256 && lanes != 1024) return set_error(ZR_INVALID_INPUT, "encoder width must be 256 or 1024");
+    g_enc_width.store(lanes, std::memory_order_relaxed);
+    return ZR_OK;
+}
+
 int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches) {
     ZR_GUARD_BEGIN
     clear_error();
@@ -3138,7 +3141,7 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         // CU) where whole workgroups of streams fill the buffers: measured in
         // round 4 at -3 % encoder time but +13 % in the
         // compaction that follows, so the 256-lane shape stays the default and
-        // ZR_ENC_W=1024 selects the other (tests and A/B runs)
+        // zr_rans_set_encoder_width(1024) selects the other
         const bool wide = enc_w1024() && !narrow && a.N % 1024 == 0;
         if (narrow)
             launch_timed("rans_encode", w.il ? k_enc_xn<64, 0, true> : k_enc_xn<64, 0, false>,
