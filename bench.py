@@ -46,6 +46,11 @@ def parse():
     p.add_argument("--groups", type=int, default=1,
                    help="rans: code the buffers as G groups on G HIP streams after the shared table "
                         "(encode+compaction+decode of one group overlap the others')")
+    p.add_argument("--pipeline", action="store_true",
+                   help="rans: two distinct batches alternate; each step codes one (encode -> decode on the "
+                        "main stream) while the histogram + table of the next one run on a second stream")
+    p.add_argument("--enc-width", type=int, default=256, choices=[256, 1024],
+                   help="rans: the xN encoder's workgroup width (zr_rans_set_encoder_width)")
     p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--fse-block-kib", type=int, default=64)
     p.add_argument("--dry-run", action="store_true",
@@ -161,7 +166,10 @@ def pmc_traffic(workload, kernel):
         return None, None
     with open(TRAFFIC_FILE) as fh:
         doc = json.load(fh)
-    t = doc.get("workloads", {}).get(workload, {}).get(kernel)
+    wl = doc.get("workloads", {}).get(workload, {})
+    t = wl.get(kernel)
+    if t is None and kernel == "k_enc_compact_reg":  # (the literal config keeps the LDS-image compaction)
+        t = wl.get("k_enc_compact_lds")
     src = f"profiles/traffic.json ({doc.get('source', '?')})"
     return (round(t["hbm_bytes"]) if t else None), src
 
@@ -288,7 +296,7 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
     return res
 
 
-RANS_SYMS = {"rans_encode": "k_enc_xn", "rans_decode": "k_dec_xn_fast", "rans_compact": "k_enc_compact_lds",
+RANS_SYMS = {"rans_encode": "k_enc_xn", "rans_decode": "k_dec_xn_fast", "rans_compact": "k_enc_compact_reg",
              "histogram": "k_hist"}
 KMS_SOURCE = ("instrumented passes before the timed region (8 steps per kernel, that kernel alone HIP-event "
               "timed on every 4th step); the roofline's avg_launch_ms is the dominant kernel's, timed alone on "
@@ -616,11 +624,16 @@ def run_blob(args, torch, dist, world, rank, dev, zr, L):
 
     comm = zd.shared_table_comm(world, rank) if world > 1 else None  # the shared trained table over ranks
 
+    fused = comm is None and hasattr(L, "zr_rans_dtab_from_data_dev")  # histogram + table in one launch
+
     def step():
-        bt.histogram(raw)
-        if comm is not None:
-            comm.allreduce_histogram(bt.hist)
-        bt.tables_from_hist()
+        if fused:
+            bt.table_from_data(raw)
+        else:
+            bt.histogram(raw)
+            if comm is not None:
+                comm.allreduce_histogram(bt.hist)
+            bt.tables_from_hist()
         bt.encode(raw, enc)
         bt.decode(enc, out)
 
@@ -726,7 +739,35 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     # histogram workgroup); more ranks: the all-reduce sits between the two
     fused = comm is None and hasattr(L, "zr_rans_dtab_from_data_dev")
 
+    # --pipeline: batches A and B (distinct data) alternate. Step k codes batch
+    # k % 2 with the table made in step k - 1, and on a second stream makes the
+    # table of batch (k + 1) % 2 once step k - 1 is done with it: the
+    # histogram's HBM pass runs beside the latency-bound encoder
+    pipe = bool(getattr(args, "pipeline", False)) and G == 1 and fused
+    if pipe:
+        host_b = zr.synth(args.kind, total, seed=0x2545F4914F6CDD1D + rank)
+        raw_b = torch.frombuffer(bytearray(host_b), dtype=torch.uint8).to(dev)
+        bt_b = RansDeviceBatch([n] * B, N, device=dev, shared_table=True)
+        pp = {"k": 0, "batches": [(bt, raw), (bt_b, raw_b)], "side": torch.cuda.Stream(dev),
+              "tab": [torch.cuda.Event(), torch.cuda.Event()], "done": [torch.cuda.Event(), torch.cuda.Event()]}
+        bt.table_from_data(raw, stream)
+        pp["tab"][0].record(stream)
+
     def step():
+        if pipe:
+            k = pp["k"]
+            x, y = k & 1, (k & 1) ^ 1
+            (bx, rx), (by, ry) = pp["batches"][x], pp["batches"][y]
+            side = pp["side"]
+            side.wait_event(pp["done"][y])  # step k - 1 has finished with batch y's table
+            by.table_from_data(ry, side)
+            pp["tab"][y].record(side)
+            stream.wait_event(pp["tab"][x])
+            bx.encode(rx, enc, stream)
+            bx.decode(enc, out, stream)
+            pp["done"][x].record(stream)
+            pp["k"] = k + 1
+            return
         if fused:
             bt.table_from_data(raw, stream)
         else:
@@ -746,11 +787,17 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
         for *_, st in groups:
             stream.wait_stream(st)
 
+    def last_raw():  # the batch the last step decoded (and its status array)
+        if not pipe:
+            return bt, raw
+        return pp["batches"][(pp["k"] - 1) & 1]
+
     step()
     torch.cuda.synchronize(dev)
     if not diag:
-        bt.raise_on_error()
-        if not torch.equal(out, raw):
+        b_, r_ = last_raw()
+        b_.raise_on_error()
+        if not torch.equal(out, r_):
             raise SystemExit("decode mismatch after the first step")
 
     dt, dom, dom_ms, kms, tms = _measure(torch, dist, world, dev, L, step, args,
@@ -758,9 +805,19 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
                                          also=["rans_decode"])
 
     if not diag:
-        bt.raise_on_error()
-        if not torch.equal(out, raw):
+        b_, r_ = last_raw()
+        b_.raise_on_error()
+        if not torch.equal(out, r_):
             raise SystemExit("decode mismatch in timed region")
+        if pipe:  # the other batch, coded once more on its own
+            b2, r2 = pp["batches"][pp["k"] & 1]
+            torch.cuda.synchronize(dev)
+            b2.encode(r2, enc, stream)
+            b2.decode(enc, out, stream)
+            torch.cuda.synchronize(dev)
+            b2.raise_on_error()
+            if not torch.equal(out, r2):
+                raise SystemExit("decode mismatch (second pipelined batch)")
     if G > 1:  # the groups' statuses and lengths
         for sub, *_ in groups:
             sub.raise_on_error()
@@ -798,7 +855,10 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
                                 f"rANS O0 encode+decode, {total >> 20} MiB uniform bytes per GPU as "
                                 f"{B} x {n >> 20} MiB buffers, {N}-way interleaved streams each "
                                 f"({B * N} streams), shared table (histogram all-reduce over ranks)"),
-                   "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}"},
+                   "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}",
+                   **({"pipelined": "two distinct 256 MiB batches alternate; step k codes one batch (encode -> "
+                                    "decode) while the histogram + table of the other run on a second HIP stream"}
+                      if pipe else {})},
         # the dominant kernel's roofline (the encoder on the headline): algorithmic bytes
         # per launch = N_in read + C written (encode, decode), 2 C (compaction), N_in (histogram)
         "roofline": _roofline(dom, dom_ms, rans_bytes, wl, RANS_SYMS, kms),
@@ -947,6 +1007,8 @@ def main():
     import zipora_amd as zr
     L = zr.load()
     L.zr_set_device(local)
+    if hasattr(L, "zr_rans_set_encoder_width") and L.zr_rans_set_encoder_width(args.enc_width):
+        raise SystemExit(f"encoder width {args.enc_width} refused")
 
     copy_ceiling(torch, dev, L)
     if args.workload in ("fse", "o1", "blob"):

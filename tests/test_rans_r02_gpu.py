@@ -634,7 +634,8 @@ def test_wide_decode_errors_grid_beyond_residency(zr, oracle):
     assert check(*run(host, enc_len), host, enc_len) >= 16
 
 
-@pytest.mark.parametrize("kind,B,n", [("u", 64, 4 << 20), ("t", 3, 100_000), ("z", 1, 5000), ("u", 1, 0)])
+@pytest.mark.parametrize("kind,B,n", [("u", 64, 4 << 20), ("t", 3, 100_000), ("z", 1, 5000), ("u", 1, 0),
+                                      ("t", 3000, 1000)])  # (the last: records, k_hist_small's fused form)
 def test_table_from_data_fused(zr, oracle, kind, B, n):
     """zr_rans_dtab_from_data_dev (histogram + table build in the last k_hist
     workgroup): the table equals the oracle's

@@ -10,7 +10,7 @@ W = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 K = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 H = 1 + W + 32 + K
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-names = ["k_hist", "k_tab", "k_enc_xn<256", "k_enc_compact_lds", "k_dec_xn_fast<1024"]
+names = ["k_hist", "k_tab", "k_enc_xn<", "k_enc_compact", "k_dec_xn_fast<1024"]
 print("kernel trace of `python3 bench.py` (the default command): per-dispatch durations, us")
 print(f"headline: the first {H} dispatches of each kernel (1 first step + {W} warmup + 4x8 instrumented"
       f" + {K} timed); the timed region is dispatches {H - K + 1}-{H}")

@@ -75,6 +75,16 @@ __host__ __device__ inline uint32_t enc_rsh(uint32_t f) { return f <= 1 ? 0u : 3
 __host__ __device__ inline uint32_t enc_rcp(uint32_t f) {
     return f ? (uint32_t)(((1ull << (24 + enc_rsh(f))) + f - 1) / f) : 0u;
 }
+// enc_rcp without a 64-bit division (device table builds): the quotient of
+// the exact doubles 2^(24 + rsh) + f - 1 (< 2^37) and f, truncated, then
+// corrected to the floor (the rounded quotient is at most one above it)
+__device__ inline uint32_t enc_rcp_fast(uint32_t f) {
+    if (!f) return 0u;
+    const uint64_t num = (1ull << (24 + enc_rsh(f))) + f - 1;
+    uint64_t q = (uint64_t)((double)num / (double)f);
+    q -= q * f > num;
+    return (uint32_t)q;
+}
 __host__ __device__ inline uint32_t enc_div(uint32_t x, uint32_t rcp, uint32_t rsh) {
     return (uint32_t)(((uint64_t)(x << 8) * rcp) >> 32) >> rsh;
 }
