@@ -168,8 +168,6 @@ def pmc_traffic(workload, kernel):
         doc = json.load(fh)
     wl = doc.get("workloads", {}).get(workload, {})
     t = wl.get(kernel)
-    if t is None and kernel == "k_enc_compact_reg":  # (the literal config keeps the LDS-image compaction)
-        t = wl.get("k_enc_compact_lds")
     src = f"profiles/traffic.json ({doc.get('source', '?')})"
     return (round(t["hbm_bytes"]) if t else None), src
 
@@ -296,7 +294,7 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
     return res
 
 
-RANS_SYMS = {"rans_encode": "k_enc_xn", "rans_decode": "k_dec_xn_fast", "rans_compact": "k_enc_compact_reg",
+RANS_SYMS = {"rans_encode": "k_enc_xn", "rans_decode": "k_dec_xn_fast", "rans_compact": "k_enc_compact_lds",
              "histogram": "k_hist"}
 KMS_SOURCE = ("instrumented passes before the timed region (8 steps per kernel, that kernel alone HIP-event "
               "timed on every 4th step); the roofline's avg_launch_ms is the dominant kernel's, timed alone on "

@@ -495,12 +495,6 @@ static bool enc_w1024() { return g_enc_width.load(std::memory_order_relaxed) == 
 #ifndef ZR_ENC_PF
 #define ZR_ENC_PF 1
 #endif
-#ifndef ZR_X1_W8
-#define ZR_X1_W8 1  // k_dec_x1_fast with 8-byte slot entries
-#endif
-#ifndef ZR_CMP_REG
-#define ZR_CMP_REG 1  // the register compaction for lane-interleaved scratch
-#endif
 template <uint32_t EW, int ABL, bool IL>
 __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
     // DB: two input tiles, written alternately, so one barrier per tile
@@ -944,78 +938,6 @@ __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, Ra
     }
 }
 
-
-// Stream compaction straight from registers (rans.rs:402-419; lane-interleaved
-// scratch, the 256-lane or 1024-lane encoder's stream offsets): one lane per
-// stream, one 256-lane workgroup per 256-stream block. A lane copies its
-// stream's 16-B scratch quads to their destination e + 12 N + offset + 16 q:
-// the loads of a wave read one 1-KiB run per quad row (the interleaved layout),
-// the stores are 16-B global stores at the stream's byte alignment (the
-// hardware takes unaligned global accesses), each lane filling its own
-// destination lines in order; a stream's last partial quad leaves as bytes, so
-// no lane writes a byte of another stream. No LDS, no windows. CQ quads in
-// flight per lane.
-template <uint32_t CQ>
-__global__ __launch_bounds__(256) void k_enc_compact_reg(uint8_t *enc, KArgs a, RansWork w) {
-    const uint32_t nblk = w.nblk;
-    const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x % nblk;
-    if (b >= a.B) return;
-    const uint64_t n = a.len[b];
-    const uint32_t N = a.N;
-    if (single_mode(n, N)) return;
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    // every wave: the bytes of the blocks below this one (<= SCAN_FUSE block sums),
-    // and whether the encoder flagged any block of the buffer
-    const uint64_t v = lane < nblk ? w.blocksum[(size_t)b * nblk + lane] : 0;
-    const uint64_t c = v & ~BS_ERR;
-    const uint64_t below = wave_sum(lane < blk ? c : 0);
-    const bool flagged = __any((v >> 63) != 0);
-    const uint64_t tot = wave_sum(c);
-    if (blk == 0 && tid == 0) {  // the only status writer of an xN encode
-        a.enc_len[b] = (uint64_t)N * 12 + tot;
-        a.status[b] = flagged ? ZR_INVALID_INPUT : ZR_OK;
-    }
-    if (flagged) return;
-    const uint32_t s = blk * 256 + tid;
-    if (s >= N) return;
-    const uint32_t L = w.st_len[(size_t)b * N + s];
-    const uint64_t off = below + w.st_off[(size_t)b * N + s];
-    const uint32_t X = w.st_state[(size_t)b * N + s];
-    uint8_t *const e = enc + a.enc_off[b];
-    if ((((uintptr_t)e) & 7) == 0) {
-        *reinterpret_cast<uint2 *>(e + 8 * (size_t)s) = make_uint2(X, 0);
-        *reinterpret_cast<uint32_t *>(e + 8 * (size_t)N + 4 * (size_t)s) = L;
-    } else {
-        st_u32_u(e + 8 * (size_t)s, X);
-        st_u32_u(e + 8 * (size_t)s + 4, 0);
-        st_u32_u(e + 8 * (size_t)N + 4 * (size_t)s, L);
-    }
-    uint8_t *const dst = e + 12 * (size_t)N + off;
-    const uint8_t *const src = w.scratch + (size_t)b * w.region + (size_t)(s - lane) * w.cap + lane * 16;
-    const uint32_t full = L >> 4;  // whole quads
-    uint32_t q = 0;
-    for (; q + CQ <= full; q += CQ) {
-        v4u t[CQ];
-#pragma unroll
-        for (uint32_t k = 0; k < CQ; k++) t[k] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(src + (size_t)(q + k) * 1024));
-        uint8_t *p = dst + 16 * (size_t)q;
-#pragma unroll
-        for (uint32_t k = 0; k < CQ; k++)  // (one address, immediate offsets)
-            asm volatile("global_store_dwordx4 %0, %1, off offset:%2" ::"v"(p), "v"(t[k]), "i"(16 * k) : "memory");
-    }
-    for (; q < full; q++) {
-        const v4u t = *reinterpret_cast<const v4u *>(src + (size_t)q * 1024);
-        uint8_t *p = dst + 16 * (size_t)q;
-        asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(t) : "memory");
-    }
-    const uint32_t tail = L & 15;
-    if (tail) {
-        const v4u t = *reinterpret_cast<const v4u *>(src + (size_t)full * 1024);
-        const uint32_t wd[4] = {t.x, t.y, t.z, t.w};
-        uint8_t *p = dst + 16 * (size_t)full;
-        for (uint32_t i = 0; i < tail; i++) p[i] = (uint8_t)(wd[i >> 2] >> (8 * (i & 3)));
-    }
-}
 
 // Stream compaction through an LDS image of the destination (rans.rs:402-419):
 // the CS consecutive streams of a group are contiguous in the destination.
@@ -2683,32 +2605,15 @@ constexpr uint32_t NSET = 1;   // staging register sets: a refill lands NSET bou
 // decodes, 0 for the other x1 records (k_dec_x1_ring's), so that kernel need not
 // re-derive x1_fast_ok (the records' offsets and final states: 134 MB of reads
 // for a million records)
-// W8 (round 4): 8-byte slot entries {f | sym << 24, slot - start} as the
-// headline decoder's (the update one mad_u24 on the entry, the symbol its top
-// byte): 32 KiB of table, so the 32-row ring has no mirror row (the window's
-// two rows read separately, the second wrapped by one AND)
-template <bool W8>
 __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t *raw, KArgs a, uint32_t *taken) {
-    constexpr uint32_t TABW = (W8 ? 2 : 1) * TOTFREQ;
-    constexpr bool MIR = !W8;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[TABW + (RR + (MIR ? 1 : 0)) * XF];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[TOTFREQ + (RR + 1) * XF];
     const uint32_t tid = threadIdx.x;
-    uint32_t *const lring = lds + TABW + tid;
+    uint32_t *const lring = lds + TOTFREQ + tid;
     const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
     {
         const v4u *src = reinterpret_cast<const v4u *>(T->slot);
         v4u *dst = reinterpret_cast<v4u *>(lds);
-        for (uint32_t j = tid; j < TOTFREQ / 4; j += XF) {
-            const v4u q = src[j];
-            if constexpr (W8) {
-                auto wide = [](uint32_t e) -> v2u { return v2u{(e >> 20) | (e << 24), (e >> 8) & 0xFFF}; };
-                const v2u w0 = wide(q.x), w1 = wide(q.y), w2 = wide(q.z), w3 = wide(q.w);
-                dst[2 * j] = v4u{w0.x, w0.y, w1.x, w1.y};
-                dst[2 * j + 1] = v4u{w2.x, w2.y, w3.x, w3.y};
-            } else {
-                dst[j] = q;
-            }
-        }
+        for (uint32_t j = tid; j < TOTFREQ / 4; j += XF) dst[j] = src[j];
     }
     const bool normal = T->kind == DT_NORMAL;
     __syncthreads();
@@ -2748,7 +2653,7 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
         p[4 * XF] = c1.x; p[5 * XF] = c1.y; p[6 * XF] = c1.z; p[7 * XF] = c1.w;
         p[8 * XF] = c2.x; p[9 * XF] = c2.y; p[10 * XF] = c2.z; p[11 * XF] = c2.w;
         p[12 * XF] = c3.x; p[13 * XF] = c3.y; p[14 * XF] = c3.z;
-        if (MIR) p[15 * XF] = c3.w;                  // row 16, or the mirror row 32
+        p[15 * XF] = c3.w;                           // row 16, or the mirror row 32
         lring[((r0 + 15) & (RR - 1)) * XF] = c3.w;  // row 0 itself (r0 = 17; r0 = 1: row 16 again)
     };
     // prologue: the 64-B segment holding the record's last stream byte and the one below
@@ -2768,27 +2673,15 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
     uint32_t x = fast ? (uint32_t)X : RANS_L;
     bool bad = false;
     auto readD = [&](uint32_t p8) -> uint32_t {  // the 4 stream bytes below p (byte p-1 on top)
-        if constexpr (!MIR) {  // rows r and r + 1 (mod 32)
-            const uint32_t o0 = (p8 << 7) & ((RR - 1) * XF * 4), o1 = (o0 + XF * 4) & ((RR - 1) * XF * 4);
-            const char *base = reinterpret_cast<const char *>(lds + TABW) + tid * 4;
-            return __builtin_amdgcn_alignbit(*reinterpret_cast<const uint32_t *>(base + o1),
-                                             *reinterpret_cast<const uint32_t *>(base + o0), p8);
-        }
         const uint32_t *q = lring + ((p8 >> 5) & (RR - 1)) * XF;
         return __builtin_amdgcn_alignbit(q[XF], q[0], p8);
     };
-    // one decode step (rans.rs:472-507), as in k_dec_xn_fast; W8: the entry
-    // with the symbol in its top byte
+    // one decode step (rans.rs:472-507), as in k_dec_xn_fast
     auto step = [&](uint32_t D, uint32_t &hi, uint32_t &lo, uint32_t &sft) -> uint32_t {
         sft = __builtin_clz(x) & 24;
         const uint64_t t = ((((uint64_t)x) << 32) | D) << sft;
         hi = (uint32_t)(t >> 32);
         lo = (uint32_t)t;
-        if constexpr (W8) {
-            const v2u e2 = *reinterpret_cast<const v2u *>(reinterpret_cast<const char *>(lds) + ((hi >> 5) & 0x7FF8));
-            x = __umul24(e2.x, hi >> 20) + e2.y;
-            return e2.x;
-        }
         const uint32_t ent =
             *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + ((hi >> 6) & 0x3FFC));
         x = __umul24(ent >> 20, hi >> 20) + ((ent >> 8) & 0xFFF);
@@ -2845,7 +2738,7 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
             // sym A | sym B << 8, packed as soon as the pair is done (an empty asm
             // pins it: left to the scheduler, all 16 entries stay live to the
             // tile's end)
-            uint32_t pr = __builtin_amdgcn_perm(eB, eA, W8 ? 0x0c0c0703u : 0x0c0c0400u);
+            uint32_t pr = __builtin_amdgcn_perm(eB, eA, 0x0c0c0400u);
             asm volatile("" : "+v"(pr));
             if (j & 1)
                 o[j >> 1] = __builtin_amdgcn_perm(pr, lo2, 0x05040100u);
@@ -2853,15 +2746,6 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
                 lo2 = pr;
         }
         if constexpr (!decltype(irr)::value) pos_snap = pos8;
-    };
-    // every memory operation done (the staging registers tied to the wait; the
-    // second set only exists with NSET = 2: tying it otherwise kept 16 VGPRs live)
-    auto wait_all = [&]() {
-        if constexpr (NSET == 2)
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1),
-                         "+v"(f2), "+v"(f3)::"memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
     };
     // memory operations younger than the loads being waited for: NSET = 2, the 4
     // loads of boundary t - 1 (+ the previous group's XG stores at the first two
@@ -2915,7 +2799,8 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
                 }
             }
             // per-lane stores: resynchronise the vmcnt accounting
-            wait_all();
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1),
+                         "+v"(f2), "+v"(f3)::"memory");
         }
     };
     const uint32_t nreg = cmin / (16 * XG);  // groups in which every fast lane of the wave is live
@@ -2924,12 +2809,13 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
     for (; g < ngrp; g++) group(g, std::true_type());
     // the reads of the wave's last tile (lanes live in it)
     bad |= fast && 16 * (ntile - 1) < nn && (int32_t)(pos8 - 32 - ((uint32_t)lo64 << 3)) < 0;
-    wait_all();
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1), "+v"(f2),
+                 "+v"(f3)::"memory");
     if (fast) {
         int32_t st;
         if (bad) {
             atomicAdd(&g_dec_fallbacks, 1ull);
-            st = x1_dec_generic(T, W8 ? T->slot : lds, normal, e, len, X, out, n) ? ZR_OK : ZR_INVALID_INPUT;
+            st = x1_dec_generic(T, lds, normal, e, len, X, out, n) ? ZR_OK : ZR_INVALID_INPUT;
         } else {
             // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
             const uint32_t consumed = (((uint32_t)pend << 3) - pos_snap) >> 3;
@@ -3322,9 +3208,6 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             // the 256-lane encoder leaves each stream's offset in its block (a
             // block's bytes fit 32 bits: 256 * cap < 2^32)
             const int has_off = !narrow && 256ull * w.cap < (1ull << 32);
-            if (ZR_CMP_REG && has_off && w.il && w.nblk <= SCAN_FUSE)
-                launch_timed("rans_compact", k_enc_compact_reg<8>, dim3((uint32_t)gx), dim3(256), 0, s, enc, a, w);
-            else
             launch_timed("rans_compact", kcmp, dim3((uint32_t)(gx * 16 * nwin)), dim3(256), 0, s, enc, a, w, nwin,
                          has_off);
         }
@@ -3426,7 +3309,7 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
             // k_dec_x1_fast takes the records x1_fast_ok admits, k_dec_x1_ring the rest
             // one workgroup per CU (148 KiB of LDS each), persistent waves
             const uint64_t gf = std::min<uint64_t>(ceil_div(a.B, XF), (uint64_t)cu_count());
-            hipLaunchKernelGGL(k_dec_x1_fast<ZR_X1_W8 != 0>, dim3((uint32_t)gf), dim3(XF), 0, s, enc, raw, a,
+            hipLaunchKernelGGL(k_dec_x1_fast, dim3((uint32_t)gf), dim3(XF), 0, s, enc, raw, a,
                                w.st_state);
             hipLaunchKernelGGL(k_dec_x1_ring, dim3((uint32_t)ceil_div(a.B, X1W)), dim3(X1W), 0, s, enc, raw, a,
                                (const uint32_t *)w.st_state);
