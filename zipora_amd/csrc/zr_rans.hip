@@ -495,6 +495,27 @@ static bool enc_w1024() { return g_enc_width.load(std::memory_order_relaxed) == 
 #ifndef ZR_ENC_PF
 #define ZR_ENC_PF 1
 #endif
+#ifndef ZR_ENC_V2
+#define ZR_ENC_V2 1
+#endif
+// V2 encode entry of symbol v (freq f): {f << 12 (0: not in table), two-byte
+// threshold (f << 4, 0xFFFF = never) << 16 | start', R, cmpl | sh << 24} with
+// q = umulhi(y, R) >> sh = y / f exact for y < 2^24 (R = ceil(2^(32+sh) / f),
+// sh = ceil(log2 f) - 1, so R < 2^32 and R f - 2^(32+sh) < f <= 2^(8+sh)).
+// f = 1 has no such R: R = 2^32 - 1 gives q = y - 1 (y >= 1 after renorm) and
+// start' = start + 4095 puts the missing 4095 = cmpl back.
+__device__ __forceinline__ uint4 enc_entry_v2(uint32_t f, uint32_t start) {
+    uint32_t R = 0, sh = 0, st = start;
+    if (f == 1) {
+        R = 0xFFFFFFFFu;
+        st += 4095;
+    } else if (f >= 2) {
+        sh = 31 - __builtin_clz(f - 1);
+        R = (uint32_t)(((1ull << (32 + sh)) + f - 1) / f);
+    }
+    const uint32_t t2 = f == 0 ? 0u : (f < 16 ? f << 4 : 0xFFFFu);
+    return make_uint4(f << 12, (t2 << 16) | st, R, ((TOTFREQ - f) & 0xFFF) | (sh << 24));
+}
 template <uint32_t EW, int ABL, bool IL>
 __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
     // DB: two input tiles, written alternately, so one barrier per tile
@@ -546,10 +567,16 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // one byte if > low half ((freq << 4) - 1), two if > high half ((freq << 12) - 1,
     // 0xFFFF = never, freq >= 16); y = start << 8; z = reciprocal;
     // w = (4096 - freq) << 8 | rsh << 24 (mad_u24 reads the low 24 bits)
+    // V2 (ZR_ENC_V2): the state is x itself and the entry is enc_entry_v2's
+    constexpr bool V2 = ZR_ENC_V2 != 0;
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
     for (uint32_t i = tid; i < 256 * TC; i += EW) {
         const uint32_t v = i / TC;
         const uint32_t f = T->freq[v];
+        if constexpr (V2) {
+            et[i] = enc_entry_v2(f, T->start[v]);
+            continue;
+        }
         const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
         et[i] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
                            (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
@@ -590,9 +617,10 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     auto dword = [&](uint32_t d) -> uint32_t * {
         return reinterpret_cast<uint32_t *>(qbase + (d >> 2) * qstride + (d & 3) * 4);
     };
-    uint32_t X = RANS_L << 8;
+    uint32_t X = V2 ? RANS_L : RANS_L << 8;
     uint64_t acc = 0;   // pending output bits (emission order from bit 0)
     uint32_t nacc = 0;  // valid bits in acc, < 32 after every push
+    uint32_t P = 0;     // V2: output bits so far (the ring holds them in place)
     bool err = false;
     uint32_t xmin = 0xFFFFFFFFu;  // min F over coded symbols: 0 = a symbol not in the table
     // encode_symbol (rans.rs:303-335), branchless: at most two renorm bytes
@@ -606,6 +634,23 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         return xh > (F >> 16) ? 16u : (xh > (F & 0xFFFFu) ? 8u : 0u);
     };
     auto enc = [&](const uint4 e, bool valid, uint32_t &nb) -> uint32_t {
+        if constexpr (V2) {
+            // x >= f << 12: one byte; x >= f << 20 <=> (x >> 16) >= f << 4: two
+            const uint32_t n1 = X >= e.x ? 8u : 0u;
+            nb = valid ? ((X >> 16) >= (e.y >> 16) ? 16u : n1) : 0u;
+            const uint32_t bits = __builtin_amdgcn_ubfe(X, 0, nb);
+            const uint32_t y = X >> nb;
+            const uint32_t q = __umulhi(y, e.z) >> (e.w >> 24);
+            // x' = q * cmpl + y + start' (mad_u24 reads w's low 24 bits; start'
+            // is the low half of y's word, added by SDWA, no extraction)
+            uint32_t xn;
+            asm("v_mad_u32_u24 %0, %1, %2, %3\n\t"
+                "v_add_u32_sdwa %0, %0, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                : "=&v"(xn)
+                : "v"(q), "v"(e.w), "v"(y), "v"(e.y));
+            X = valid ? xn : X;
+            return bits;
+        }
         nb = valid ? renorm_bits(e.x) : 0u;
         const uint32_t bits = __builtin_amdgcn_ubfe(X, 8, nb);
         const uint32_t Y = X >> nb;
@@ -633,8 +678,26 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     uint32_t ra16 = tid * 4;  // (W16: only ever written by 16-bit ops, so < 2^16)
     uint32_t nfl = 0;                 // dwords moved to scratch
     // two steps' bits (A first) -> acc, then the ring
+    // V2: the pair's bits go straight to their place: OR-ed into the partial
+    // dword (row P >> 5), the overflow written to the next row, which no bit
+    // has reached yet (so a plain write also clears what the ring held there)
     auto push2 = [&](uint32_t bA, uint32_t nbA, uint32_t bB, uint32_t nbB) {
         const uint32_t cpair = bA | (bB << nbA);  // <= 32 bits
+        if constexpr (V2) {
+            const uint64_t v = (uint64_t)cpair << (P & 31);
+            // row P >> 5 of this lane: (P << (log2 ROW - 5)) & row mask | tid * 4
+            // (one v_and_or); the next row wraps by an AND
+            uint32_t alo, ahi;
+            asm("v_lshlrev_b32 %0, %1, %2\n\tv_and_or_b32 %0, %0, %3, %4"
+                : "=&v"(alo)
+                : "i"(__builtin_ctz(ROW) - 5), "v"(P), "s"((RING_BYTES - 1) & ~(ROW - 1)), "v"(tid * 4));
+            ahi = (alo + ROW) & (RING_BYTES - 1);
+            __hip_atomic_fetch_or(static_cast<uint32_t *>(__builtin_assume_aligned(lds + alo, 4)), (uint32_t)v, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            *reinterpret_cast<uint32_t *>(lds + ahi) = (uint32_t)(v >> 32);
+            P += nbA + nbB;
+            return;
+        }
         acc |= (uint64_t)cpair << nacc;
         nacc += nbA + nbB;  // < 64
         if constexpr (W16) {
@@ -656,6 +719,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // dwords completed: counted (nw32), or (W16) the flushed ones plus the ring
     // rows from the flushed row to ra's (fewer than ERS are ever pending)
     auto nw_of = [&]() -> uint32_t {
+        if constexpr (V2) return P >> 5;
         if constexpr (W16) return nfl + ((ra16 / ROW - nfl) & (ERS - 1));
         return nw32 >> 5;
     };
@@ -749,6 +813,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         }
     };
     const uint64_t ntiles = (cmax + ETILE - 1) / ETILE;
+    if constexpr (V2) ring[tid] = 0u;  // row 0: the first partial dword
     __syncthreads();  // the encode table
     v4u pend = issue_piece(ntiles - 1);
     // the tile loop, top tile first. Tiles ntiles-2 .. 1 are full for every
@@ -784,16 +849,28 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
             tile_fast(tl);
         } else {
             // general tile: rows past a stream's end or lanes without a stream
-            // leave the state and emit nothing
-            for (uint32_t r = rtop; r-- > 0;) {
+            // leave the state and emit nothing. Steps pushed in pairs (an odd
+            // top row alone): every push but a tile's last adds <= 7 dwords in
+            // all, which V2's overflow write (one row ahead) relies on
+            auto gstep = [&](uint32_t r, uint32_t &nb) -> uint32_t {
                 const uint64_t k = t * ETILE + r;
                 const uint32_t sym = tl[r * EW + tid];
                 const uint4 e = ent(sym);
                 const bool valid = active && k < c;
                 err |= valid && e.x == 0;  // "Symbol {} not in frequency table" (rans.rs:311-316)
+                return enc(e, valid, nb);
+            };
+            uint32_t r = rtop;
+            if (r & 1) {
                 uint32_t nb;
-                const uint32_t bits = enc(e, valid, nb);
+                const uint32_t bits = gstep(--r, nb);
                 push2(bits, nb, 0u, 0u);
+            }
+            for (; r > 0; r -= 2) {
+                uint32_t nA, nB;
+                const uint32_t bA = gstep(r - 1, nA);
+                const uint32_t bB = gstep(r - 2, nB);
+                push2(bA, nA, bB, nB);
             }
         }
     }
@@ -809,13 +886,17 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         }
         for (; nfl < nw; nfl++) *dword(nfl) = r[(nfl & (ERS - 1)) * EW];
     }
-    if (nacc) *dword(nw) = (uint32_t)acc;
+    if constexpr (V2) {
+        if (P & 31) *dword(nw) = ring[(nw & (ERS - 1)) * EW + tid];
+    } else if (nacc) {
+        *dword(nw) = (uint32_t)acc;
+    }
     // "Symbol {} not in frequency table" (rans.rs:311-316): flagged in the top bit
     // of the block's byte sum (BS_ERR); the compaction turns it into the status
     const bool bad = err || xmin == 0;
-    const uint32_t bytes = nw * 4 + nacc / 8;
+    const uint32_t bytes = nw * 4 + (V2 ? (P & 31) : nacc) / 8;
     if (active) {
-        w.st_state[(size_t)b * N + s] = X >> 8;
+        w.st_state[(size_t)b * N + s] = V2 ? X : X >> 8;
         w.st_len[(size_t)b * N + s] = bytes;
     }
     // byte sum of each 256-stream block (the unit of the offset scan); the
