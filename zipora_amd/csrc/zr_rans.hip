@@ -567,8 +567,13 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // one byte if > low half ((freq << 4) - 1), two if > high half ((freq << 12) - 1,
     // 0xFFFF = never, freq >= 16); y = start << 8; z = reciprocal;
     // w = (4096 - freq) << 8 | rsh << 24 (mad_u24 reads the low 24 bits)
-    // V2 (ZR_ENC_V2): the state is x itself and the entry is enc_entry_v2's
-    constexpr bool V2 = ZR_ENC_V2 != 0;
+    // V2 (ZR_ENC_V2): the state is x itself, the entry is enc_entry_v2's and
+    // the output bits go to the ring in place. Workgroups of >= 256 lanes only:
+    // with a lone wave per SIMD (EW = 64, the long-stream shape) every
+    // instruction's latency is on the chain and V2 measured slower (literal
+    // encode 4.22 -> 4.31 ms; the V2 step alone 4.37 ms, same box)
+    constexpr bool V2 = ZR_ENC_V2 != 0 && EW >= 256;
+    constexpr bool V2O = V2;
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
     for (uint32_t i = tid; i < 256 * TC; i += EW) {
         const uint32_t v = i / TC;
@@ -683,7 +688,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // has reached yet (so a plain write also clears what the ring held there)
     auto push2 = [&](uint32_t bA, uint32_t nbA, uint32_t bB, uint32_t nbB) {
         const uint32_t cpair = bA | (bB << nbA);  // <= 32 bits
-        if constexpr (V2) {
+        if constexpr (V2O) {
             const uint64_t v = (uint64_t)cpair << (P & 31);
             // row P >> 5 of this lane: (P << (log2 ROW - 5)) & row mask | tid * 4
             // (one v_and_or); the next row wraps by an AND
@@ -719,7 +724,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // dwords completed: counted (nw32), or (W16) the flushed ones plus the ring
     // rows from the flushed row to ra's (fewer than ERS are ever pending)
     auto nw_of = [&]() -> uint32_t {
-        if constexpr (V2) return P >> 5;
+        if constexpr (V2O) return P >> 5;
         if constexpr (W16) return nfl + ((ra16 / ROW - nfl) & (ERS - 1));
         return nw32 >> 5;
     };
@@ -813,7 +818,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         }
     };
     const uint64_t ntiles = (cmax + ETILE - 1) / ETILE;
-    if constexpr (V2) ring[tid] = 0u;  // row 0: the first partial dword
+    if constexpr (V2O) ring[tid] = 0u;  // row 0: the first partial dword
     __syncthreads();  // the encode table
     v4u pend = issue_piece(ntiles - 1);
     // the tile loop, top tile first. Tiles ntiles-2 .. 1 are full for every
@@ -886,7 +891,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         }
         for (; nfl < nw; nfl++) *dword(nfl) = r[(nfl & (ERS - 1)) * EW];
     }
-    if constexpr (V2) {
+    if constexpr (V2O) {
         if (P & 31) *dword(nw) = ring[(nw & (ERS - 1)) * EW + tid];
     } else if (nacc) {
         *dword(nw) = (uint32_t)acc;
@@ -894,7 +899,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // "Symbol {} not in frequency table" (rans.rs:311-316): flagged in the top bit
     // of the block's byte sum (BS_ERR); the compaction turns it into the status
     const bool bad = err || xmin == 0;
-    const uint32_t bytes = nw * 4 + (V2 ? (P & 31) : nacc) / 8;
+    const uint32_t bytes = nw * 4 + (V2O ? (P & 31) : nacc) / 8;
     if (active) {
         w.st_state[(size_t)b * N + s] = V2 ? X : X >> 8;
         w.st_len[(size_t)b * N + s] = bytes;
@@ -2341,14 +2346,19 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     constexpr uint32_t F = ERS / 2;             // dwords per output unit
     constexpr uint32_t ROW = EW * 4;            // ring row bytes
     constexpr uint32_t RING_BYTES = ERS * ROW;  // a power of two
-    static_assert(ERS >= F + 9, "a tile adds up to 8 dwords to at most F - 1 pending and one partial");
+    static_assert(ERS >= F + 10, "a tile adds up to 8 dwords to at most F - 1 pending, one partial and the overflow row");
+    constexpr bool V2 = ZR_ENC_V2 != 0;  // k_enc_xn's V2 step and in-place output
     __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16];
-    const uint32_t *ring = reinterpret_cast<const uint32_t *>(lds);
+    uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
     uint4 *et = reinterpret_cast<uint4 *>(lds + RING_BYTES);
     const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
     const uint32_t tid = threadIdx.x;
     for (uint32_t v = tid; v < 256; v += EW) {  // the k_enc_xn table layout
         const uint32_t f = T->freq[v];
+        if constexpr (V2) {
+            et[v] = enc_entry_v2(f, T->start[v]);
+            continue;
+        }
         const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
         et[v] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
                            (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
@@ -2362,7 +2372,7 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     uint8_t *out = enc + a.enc_off[b];
     if (!x1_enc_ok(in, out, n64)) return;  // k_enc_x1_fast's
     const uint32_t n = (uint32_t)n64;
-    uint32_t X = RANS_L << 8;
+    uint32_t X = V2 ? RANS_L : RANS_L << 8;
     uint32_t xmin = 0xFFFFFFFFu;
     uint64_t acc = 0;   // pending output bits (emission order from bit 0)
     uint32_t nacc = 0;  // valid bits in acc, < 32 after every push
@@ -2370,8 +2380,21 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     uint32_t ra = tid * 4 + oal * ROW;  // + ROW * dwords completed, wrapped by one AND on use
     uint32_t nw32 = 0;                  // 32 * dwords completed
     uint32_t nfl = 0;                   // dwords stored
+    uint32_t P = 32 * oal;              // V2: output bits so far, + 32 oal (P >> 5 = the ring row)
     auto step = [&](const uint4 e, uint32_t &nb) -> uint32_t {  // see k_enc_xn
         xmin = min(xmin, e.x);
+        if constexpr (V2) {
+            const uint32_t n1 = X >= e.x ? 8u : 0u;
+            nb = (X >> 16) >= (e.y >> 16) ? 16u : n1;
+            const uint32_t bits = __builtin_amdgcn_ubfe(X, 0, nb);
+            const uint32_t y = X >> nb;
+            const uint32_t q = __umulhi(y, e.z) >> (e.w >> 24);
+            asm("v_mad_u32_u24 %0, %1, %2, %3\n\t"
+                "v_add_u32_sdwa %0, %0, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                : "=&v"(X)
+                : "v"(q), "v"(e.w), "v"(y), "v"(e.y));
+            return bits;
+        }
         const uint32_t xh = X >> 16;
         nb = xh > (e.x >> 16) ? 16u : (xh > (e.x & 0xFFFFu) ? 8u : 0u);
         const uint32_t bits = __builtin_amdgcn_ubfe(X, 8, nb);
@@ -2382,6 +2405,20 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     };
     auto push2 = [&](uint32_t bA, uint32_t nbA, uint32_t bB, uint32_t nbB) {
         const uint32_t cpair = bA | (bB << nbA);
+        if constexpr (V2) {  // dword d in ring row (d + oal) mod ERS
+            const uint64_t v = (uint64_t)cpair << (P & 31);
+            uint32_t alo;
+            asm("v_lshlrev_b32 %0, %1, %2\n\tv_and_or_b32 %0, %0, %3, %4"
+                : "=&v"(alo)
+                : "i"(__builtin_ctz(ROW) - 5), "v"(P), "s"((RING_BYTES - 1) & ~(ROW - 1)), "v"(tid * 4));
+            const uint32_t ahi = (alo + ROW) & (RING_BYTES - 1);
+            __hip_atomic_fetch_or(static_cast<uint32_t *>(__builtin_assume_aligned(lds + alo, 4)), (uint32_t)v,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            *reinterpret_cast<uint32_t *>(lds + ahi) = (uint32_t)(v >> 32);
+            P += nbA + nbB;
+            nw32 = (P - 32 * oal) & ~31u;
+            return;
+        }
         acc |= (uint64_t)cpair << nacc;
         nacc += nbA + nbB;
         *reinterpret_cast<uint32_t *>(lds + (ra & (RING_BYTES - 1))) = (uint32_t)acc;
@@ -2410,6 +2447,7 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
         }
     };
     const uint32_t full = n & ~15u;
+    if constexpr (V2) ring[(size_t)oal * EW + tid] = 0u;  // (a lane's own ring cells: no barrier)
     // the ragged top (< 16 symbols), one step at a time
     for (uint32_t i = n; i > full;) {
         uint32_t nb;
@@ -2474,9 +2512,14 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     for (uint32_t i = nfl; i < nw; i++)
         *reinterpret_cast<uint32_t *>(out + 4 * (size_t)i) = ring[((i + oal) & (ERS - 1)) * EW + tid];
     size_t nout = 4 * (size_t)nw;
+    if constexpr (V2) {
+        acc = ring[((nw + oal) & (ERS - 1)) * EW + tid];
+        nacc = P & 31;
+    }
     for (uint32_t t = 0; t < nacc / 8; t++) out[nout + t] = (uint8_t)(acc >> (8 * t));
     nout += nacc / 8;
-    for (int t = 0; t < 8; t++) out[nout + t] = (uint8_t)((uint64_t)(X >> 8) >> (8 * t));
+    const uint32_t xf = V2 ? X : X >> 8;
+    for (int t = 0; t < 8; t++) out[nout + t] = (uint8_t)((uint64_t)xf >> (8 * t));
     a.status[b] = (xmin == 0 && n) ? ZR_INVALID_INPUT : ZR_OK;  // "Symbol {} not in frequency table"
     a.enc_len[b] = nout + 8;
 }
