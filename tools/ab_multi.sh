@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 LIBS=$1; shift
 mkdir -p gpurun_out/ab
-for r in 1 2 3; do
+for r in $(seq 1 ${ROUNDS:-3}); do
   for L in $LIBS; do
     ZR_LIB_PATH=$L timeout -k 10 120 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-path "$@" \
       > gpurun_out/ab/run.log 2>&1 || { cat gpurun_out/ab/run.log; exit 1; }
