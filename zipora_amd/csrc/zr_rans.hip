@@ -519,6 +519,17 @@ __device__ __forceinline__ uint4 enc_entry_v2(uint32_t f, uint32_t start) {
 #ifndef ZR_ENC_YS
 #define ZR_ENC_YS 1
 #endif
+// a wave-uniform pointer, said so (readfirstlane), so that a per-lane 32-bit
+// offset added to it is a scalar-base load and the compiler cannot fold the
+// uniform part into a per-lane 64-bit base it multiplies every iteration
+// (in the global address space: a flat load would count in lgkmcnt)
+typedef __attribute__((address_space(1))) const uint8_t gcu8;
+__device__ __forceinline__ gcu8 *uniform_ptr(const uint8_t *base) {
+    const uint64_t p = (uint64_t)base;
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);
+    return (gcu8 *)u;
+}
 // the V2 step (state x, entry e from enc_entry_v2); returns the emitted bits,
 // nb their count. The chain from x to x' is the renorm test, y, the quotient
 // and one mad: y + start' (SDWA, start' is the low half of e.y) is formed
@@ -752,8 +763,9 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         if constexpr (W16) return nfl + ((ra16 / ROW - nfl) & (ERS - 1));
         return nw32 >> 5;
     };
+    uint32_t flim = FL * 32;  // V2O: a burst is due once P reaches (nfl + FL) * 32
     auto flush64 = [&]() {  // tile boundary: at most one 64-B burst per lane
-        const bool need = nw_of() - nfl >= FL;
+        const bool need = V2O ? P >= flim : nw_of() - nfl >= FL;
         {
             if (need) {
                 // nfl is a multiple of FL: the FL dwords are ring rows
@@ -773,6 +785,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
                     asm volatile("" ::"v"(d[0]), "v"(d[FL - 1]));
                 }
                 nfl += FL;
+                flim += FL * 32;
             }
         }
     };
@@ -806,7 +819,8 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
                 n1 = ent(sy[g - 3]);
                 n0 = ent(sy[g - 4]);
             }
-            xmin = min(xmin, min(min(c3.x, c2.x), min(c1.x, c0.x)));
+            xmin = min(min(xmin, c3.x), c2.x);  // two v_min3 per group
+            xmin = min(min(xmin, c1.x), c0.x);
             uint32_t m3, m2, m1, m0;
             const uint32_t b3 = enc(c3, true, m3);
             const uint32_t b2 = enc(c2, true, m2);
@@ -831,7 +845,8 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
                 s3 = s2 = s1 = s0 = t;
             }
             const uint4 e3 = ent(s3), e2 = ent(s2), e1 = ent(s1), e0 = ent(s0);
-            xmin = min(xmin, min(min(e3.x, e2.x), min(e1.x, e0.x)));
+            xmin = min(min(xmin, e3.x), e2.x);  // two v_min3 per group
+            xmin = min(min(xmin, e1.x), e0.x);
             uint32_t n3, n2, n1, n0;
             const uint32_t b3 = enc(e3, true, n3);
             const uint32_t b2 = enc(e2, true, n2);
@@ -848,8 +863,15 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // the tile loop, top tile first. Tiles ntiles-2 .. 1 are full for every
     // stream and their next piece is a plain 16-B load when the workgroup's
     // columns are all streams and the input is 16-B aligned.
-    const bool body_ok = vec_in && (uint64_t)(blk + 1) * EW <= N;  // workgroup-uniform
+    // (the row base of the next piece is uniform and the lane's offset in it,
+    // lr * N + col, fits 32 bits: a scalar-base load, no per-lane 64-bit
+    // multiply per tile)
+    const bool body_ok = vec_in && (uint64_t)(blk + 1) * EW <= N && (uint64_t)ETILE * N < (1ull << 32);
+    const uint32_t loff = lr * N + col;
     const bool wave_all = (uint64_t)blk * EW + (tid & ~63u) + 64 <= N;  // wave-uniform
+    // tiles t < tfast have every row below cmax - 1 (t * ETILE + ETILE < cmax):
+    // a 32-bit scalar compare per tile instead of two 64-bit ones
+    const uint32_t tfast = (uint32_t)min((cmax - 1) / ETILE, (uint64_t)0xFFFFFFFFu);
     // A one-wave workgroup (EW = 64) needs no barrier: a wave's LDS accesses
     // complete in program order (the fences pin the compiler). Wider
     // workgroups keep the shared tile: wave-private 64-column tiles split each
@@ -863,26 +885,29 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
             __builtin_amdgcn_wave_barrier();
         }
     };
-    for (uint64_t t = ntiles; t-- > 0;) {
-        uint8_t *const tl = itile + (DB ? (uint32_t)(t & 1) * ETILE * EW : 0u);
+    for (uint32_t t = (uint32_t)ntiles; t-- > 0;) {
+        uint8_t *const tl = itile + (DB ? (t & 1) * ETILE * EW : 0u);
         if (!DB) tile_sync();
         *reinterpret_cast<v4u *>(&tl[lr * EW + lp]) = pend;
         tile_sync();
-        if (body_ok && t >= 2)  // (non-temporal: same-box A/B 0.244 -> 0.238 ms)
-            pend = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(inb + ((t - 1) * ETILE + lr) * N + col));
-        else if (t > 0)
+        if (body_ok && t >= 2) {  // (non-temporal: same-box A/B 0.244 -> 0.238 ms)
+            gcu8 *rowb = uniform_ptr(inb + (uint64_t)(t - 1) * ETILE * N);
+            typedef __attribute__((address_space(1))) const v4u gcv4u;
+            pend = __builtin_nontemporal_load((gcv4u *)(rowb + loff));
+        } else if (t > 0) {
             pend = issue_piece(t - 1);
+        }
         flush64();
-        const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - t * ETILE);
-        if (rtop == ETILE && t * ETILE + ETILE < cmax && wave_all) {
+        if (t < tfast && wave_all) {
             tile_fast(tl);
         } else {
+            const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - (uint64_t)t * ETILE);
             // general tile: rows past a stream's end or lanes without a stream
             // leave the state and emit nothing. Steps pushed in pairs (an odd
             // top row alone): every push but a tile's last adds <= 7 dwords in
             // all, which V2's overflow write (one row ahead) relies on
             auto gstep = [&](uint32_t r, uint32_t &nb) -> uint32_t {
-                const uint64_t k = t * ETILE + r;
+                const uint64_t k = (uint64_t)t * ETILE + r;
                 const uint32_t sym = tl[r * EW + tid];
                 const uint4 e = ent(sym);
                 const bool valid = active && k < c;
