@@ -579,10 +579,16 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // entries over 16 quads, ~7.7 extra LDS cycles per wave-step). 64 KiB ring +
     // 64 KiB table + 32 KiB tiles = the CU's 160 KiB.
     constexpr uint32_t TC = EW == 1024 ? 16 : 1;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16 * TC + (DB ? 2 : 1) * ETILE * EW];
+    // (A linear output buffer of ERS + 1 rows re-based at each flush, so that
+    // the overflow row is an immediate offset with no wrap: 2 VALU fewer per
+    // step pair, but the row move at each flush put an LDS read -> write
+    // round trip on the wave: encoder 0.164 -> 0.173 ms, record encoder
+    // 0.675 -> 0.688 ms. Dropped.)
+    constexpr uint32_t RING_ALLOC = RING_BYTES;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_ALLOC + 256 * 16 * TC + (DB ? 2 : 1) * ETILE * EW];
     uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
-    uint4 *et = reinterpret_cast<uint4 *>(lds + RING_BYTES);
-    uint8_t *itile = lds + RING_BYTES + 256 * 16 * TC;
+    uint4 *et = reinterpret_cast<uint4 *>(lds + RING_ALLOC);
+    uint8_t *itile = lds + RING_ALLOC + 256 * 16 * TC;
     // this lane's copy, as the byte offset of entry 0 (entry v: + v * 16 * TC)
     const uint32_t et_lane = (threadIdx.x & (TC - 1)) * 16;
     auto ent = [&](uint32_t sym) -> const uint4 & {
@@ -931,17 +937,17 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // drain: the pending complete dwords (16-B pieces, then single dwords), then
     // the partial dword (its nacc / 8 whole bytes count)
     const uint32_t nw = nw_of();
+    auto rrow = [&](uint32_t d) -> uint32_t { return d & (ERS - 1); };
     {
         const uint32_t *r = ring + tid;
         while (nw - nfl >= 4) {
-            *quad(nfl >> 2) = v4u{r[(nfl & (ERS - 1)) * EW], r[((nfl + 1) & (ERS - 1)) * EW],
-                                  r[((nfl + 2) & (ERS - 1)) * EW], r[((nfl + 3) & (ERS - 1)) * EW]};
+            *quad(nfl >> 2) = v4u{r[rrow(nfl) * EW], r[rrow(nfl + 1) * EW], r[rrow(nfl + 2) * EW], r[rrow(nfl + 3) * EW]};
             nfl += 4;
         }
-        for (; nfl < nw; nfl++) *dword(nfl) = r[(nfl & (ERS - 1)) * EW];
+        for (; nfl < nw; nfl++) *dword(nfl) = r[rrow(nfl) * EW];
     }
     if constexpr (V2O) {
-        if (P & 31) *dword(nw) = ring[(nw & (ERS - 1)) * EW + tid];
+        if (P & 31) *dword(nw) = ring[rrow(nw) * EW + tid];
     } else if (nacc) {
         *dword(nw) = (uint32_t)acc;
     }
@@ -2397,9 +2403,10 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     constexpr uint32_t RING_BYTES = ERS * ROW;  // a power of two
     static_assert(ERS >= F + 10, "a tile adds up to 8 dwords to at most F - 1 pending, one partial and the overflow row");
     constexpr bool V2 = ZR_ENC_V2 != 0;  // k_enc_xn's V2 step and in-place output
-    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_BYTES + 256 * 16];
+    constexpr uint32_t RING_ALLOC = RING_BYTES;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_ALLOC + 256 * 16];
     uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
-    uint4 *et = reinterpret_cast<uint4 *>(lds + RING_BYTES);
+    uint4 *et = reinterpret_cast<uint4 *>(lds + RING_ALLOC);
     const RansDTab *T = reinterpret_cast<const RansDTab *>(a.tables);  // table 0 (stride 0)
     const uint32_t tid = threadIdx.x;
     for (uint32_t v = tid; v < 256; v += EW) {  // the k_enc_xn table layout
@@ -2431,10 +2438,10 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     uint32_t nfl = 0;                   // dwords stored
     uint32_t P = 32 * oal;              // V2: output bits so far, + 32 oal (P >> 5 = the ring row)
     auto step = [&](const uint4 e, uint32_t &nb) -> uint32_t {  // see k_enc_xn
-        xmin = min(xmin, e.x);
         if constexpr (V2) {
-            return enc_step_v2(X, e, nb);
+            return enc_step_v2(X, e, nb);  // (xmin: by the caller, min3 per pair)
         }
+        xmin = min(xmin, e.x);
         const uint32_t xh = X >> 16;
         nb = xh > (e.x >> 16) ? 16u : (xh > (e.x & 0xFFFFu) ? 8u : 0u);
         const uint32_t bits = __builtin_amdgcn_ubfe(X, 8, nb);
@@ -2471,9 +2478,10 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     // store every complete unit (one per call but for the record's first, which
     // can be short). The unit of dword nfl ends at ue; its first byte is
     // out + 4 * (ue - F), i.e. out - 4 * oal for the record's first unit
+    auto nw_of = [&]() -> uint32_t { return nw32 >> 5; };
     auto flush = [&]() {
-        const uint32_t nw = nw32 >> 5;
         for (;;) {
+            const uint32_t nw = nw_of();
             const uint32_t ue = ((nfl + oal) | (F - 1)) + 1 - oal;
             if (nw < ue) break;
             const uint32_t *r = ring + (((nfl + oal) & F) * EW) + tid;  // rows 0.. or F..
@@ -2491,7 +2499,9 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     // the ragged top (< 16 symbols), one step at a time
     for (uint32_t i = n; i > full;) {
         uint32_t nb;
-        const uint32_t bits = step(et[in[--i]], nb);
+        const uint4 e = et[in[--i]];
+        if constexpr (V2) xmin = min(xmin, e.x);
+        const uint32_t bits = step(e, nb);
         push2(bits, nb, 0u, 0u);
     }
     flush();
@@ -2508,6 +2518,10 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
             for (int g = 3; g >= 0; g--) {
                 const uint32_t w = wv[g];
                 const uint4 e3 = et[w >> 24], e2 = et[(w >> 16) & 0xFF], e1 = et[(w >> 8) & 0xFF], e0 = et[w & 0xFF];
+                if constexpr (V2) {  // two v_min3 per four steps
+                    xmin = min(min(xmin, e3.x), e2.x);
+                    xmin = min(min(xmin, e1.x), e0.x);
+                }
                 uint32_t n3, n2, n1, n0;
                 const uint32_t b3 = step(e3, n3);
                 const uint32_t b2 = step(e2, n2);
@@ -2548,12 +2562,13 @@ __global__ __launch_bounds__(EW) void k_enc_x1_ring(const uint8_t *raw, uint8_t 
     }
     // drain: the complete dwords not yet stored, the partial dword's whole bytes,
     // then the u64 state (rans.rs:362-364)
-    const uint32_t nw = nw32 >> 5;
+    const uint32_t nw = nw_of();
+    auto rrow = [&](uint32_t d) -> uint32_t { return (d + oal) & (ERS - 1); };  // ring row of dword d
     for (uint32_t i = nfl; i < nw; i++)
-        *reinterpret_cast<uint32_t *>(out + 4 * (size_t)i) = ring[((i + oal) & (ERS - 1)) * EW + tid];
+        *reinterpret_cast<uint32_t *>(out + 4 * (size_t)i) = ring[rrow(i) * EW + tid];
     size_t nout = 4 * (size_t)nw;
     if constexpr (V2) {
-        acc = ring[((nw + oal) & (ERS - 1)) * EW + tid];
+        acc = ring[rrow(nw) * EW + tid];
         nacc = P & 31;
     }
     for (uint32_t t = 0; t < nacc / 8; t++) out[nout + t] = (uint8_t)(acc >> (8 * t));
