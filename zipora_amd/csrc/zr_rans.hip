@@ -519,6 +519,9 @@ __device__ __forceinline__ uint4 enc_entry_v2(uint32_t f, uint32_t start) {
 #ifndef ZR_ENC_YS
 #define ZR_ENC_YS 1
 #endif
+#ifndef ZR_ENC_FD
+#define ZR_ENC_FD 1
+#endif
 // a wave-uniform pointer, said so (readfirstlane), so that a per-lane 32-bit
 // offset added to it is a scalar-base load and the compiler cannot fold the
 // uniform part into a per-lane 64-bit base it multiplies every iteration
@@ -770,29 +773,38 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         return nw32 >> 5;
     };
     uint32_t flim = FL * 32;  // V2O: a burst is due once P reaches (nfl + FL) * 32
-    auto flush64 = [&]() {  // tile boundary: at most one 64-B burst per lane
-        const bool need = V2O ? P >= flim : nw_of() - nfl >= FL;
-        {
-            if (need) {
-                // nfl is a multiple of FL: the FL dwords are ring rows
-                // (nfl & FL) .. +FL-1, one base address and immediate offsets
-                const uint32_t *r = ring + (nfl & FL) * EW + tid;
-                uint32_t d[FL];
+    // tile boundary: at most one burst per lane. The ring rows are read at the
+    // boundary (the tile may overwrite them), the dependent scratch stores are
+    // issued by flush_store, which the fast tile calls after its first four
+    // steps (FD, ZR_ENC_FD) so that the reads' latency overlaps the tile's own
+    uint32_t fd[FL];
+    bool fneed = false;
+    uint32_t fo = 0;
+    auto flush_read = [&]() {
+        fneed = V2O ? P >= flim : nw_of() - nfl >= FL;
+        if (fneed) {
+            // nfl is a multiple of FL: the FL dwords are ring rows
+            // (nfl & FL) .. +FL-1, one base address and immediate offsets
+            const uint32_t *r = ring + (nfl & FL) * EW + tid;
 #pragma unroll
-                for (int i = 0; i < (int)FL; i++) d[i] = r[i * EW];
-                const uint32_t o = nfl >> 2;
-                if (!(ABL & 1)) {
-                    v4u *q0 = quad(o);
+            for (int i = 0; i < (int)FL; i++) fd[i] = r[i * EW];
+            fo = nfl >> 2;
+            nfl += FL;
+            flim += FL * 32;
+        }
+    };
+    auto flush_store = [&]() {
+        if (fneed) {
+            if (!(ABL & 1)) {
+                v4u *q0 = quad(fo);
 #pragma unroll
-                    for (int k = 0; k < (int)FL / 4; k++)
-                        *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + k * qstride) =
-                            v4u{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
-                } else {
-                    asm volatile("" ::"v"(d[0]), "v"(d[FL - 1]));
-                }
-                nfl += FL;
-                flim += FL * 32;
+                for (int k = 0; k < (int)FL / 4; k++)
+                    *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(q0) + k * qstride) =
+                        v4u{fd[4 * k], fd[4 * k + 1], fd[4 * k + 2], fd[4 * k + 3]};
+            } else {
+                asm volatile("" ::"v"(fd[0]), "v"(fd[FL - 1]));
             }
+            fneed = false;
         }
     };
     // piece prefetch: plain 16-B loads one tile ahead (the compiler's own
@@ -835,6 +847,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
             const uint32_t b0 = enc(c0, true, m0);
             push2(b1, m1, b0, m0);
             c3 = n3, c2 = n2, c1 = n1, c0 = n0;
+            if (g == ETILE - 4) flush_store();
         }
     };
     auto tile_fast = [&](const uint8_t *tl) {
@@ -860,6 +873,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
             const uint32_t b1 = enc(e1, true, n1);
             const uint32_t b0 = enc(e0, true, n0);
             push2(b1, n1, b0, n0);
+            if (ZR_ENC_FD && g == ETILE - 4) flush_store();
         }
     };
     const uint64_t ntiles = (cmax + ETILE - 1) / ETILE;
@@ -903,10 +917,12 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
         } else if (t > 0) {
             pend = issue_piece(t - 1);
         }
-        flush64();
+        flush_read();
+        if (!ZR_ENC_FD) flush_store();
         if (t < tfast && wave_all) {
             tile_fast(tl);
         } else {
+            flush_store();
             const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - (uint64_t)t * ETILE);
             // general tile: rows past a stream's end or lanes without a stream
             // leave the state and emit nothing. Steps pushed in pairs (an odd
