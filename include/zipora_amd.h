@@ -170,6 +170,14 @@ int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *batc
  * workgroup per CU with 16 conflict-free copies of the encode table; used
  * where n_streams % 1024 == 0). Output bytes are identical either way. */
 int32_t zr_rans_set_encoder_width(uint32_t lanes);
+/* Tuning (no reference counterpart), process-wide: q = 1..3 codes the xN encode
+ * of a batch of at least 2^18 streams (256-lane encoder) as the encoder of the
+ * first round(B * q / 4) buffers, then the other buffers' encoder and the first
+ * part's compaction in one dispatch, then the other part's compaction; 0 runs
+ * encoder then compaction over the whole batch. Output bytes are identical. */
+int32_t zr_rans_set_encode_split(int32_t quarters);
+/* the current setting of zr_rans_set_encode_split */
+int32_t zr_rans_get_encode_split(void);
 /* bytes of device workspace needed by encode/decode of this batch geometry */
 size_t zr_rans_workspace_bytes(uint32_t n_buffers, uint32_t n_streams, uint64_t max_len);
 /* batched Rans64Encoder::encode: raw -> enc (enc + enc_off[b] must hold

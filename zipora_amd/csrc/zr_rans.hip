@@ -491,7 +491,14 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 // the xN encoder's workgroup width for batches of more than 2^16 streams
 // (zr_rans_set_encoder_width: 256, the default, or 1024 where N % 1024 == 0)
 static std::atomic<uint32_t> g_enc_width{256};
+#ifndef ZR_ENC_SPLIT_DEFAULT
+#define ZR_ENC_SPLIT_DEFAULT 0
+#endif
 static bool enc_w1024() { return g_enc_width.load(std::memory_order_relaxed) == 1024; }
+// split encode (zr_rans_set_encode_split): the xN encode of a wide batch as
+// encoder(lower half) -> encoder(upper half) + compaction(lower half) in one
+// dispatch (k_enc_cmp_fused) -> compaction(upper half)
+static std::atomic<int> g_enc_split{ZR_ENC_SPLIT_DEFAULT};
 #ifndef ZR_ENC_PF
 #define ZR_ENC_PF 1
 #endif
@@ -563,8 +570,16 @@ __device__ __forceinline__ uint32_t enc_step_v2(uint32_t &X, const uint4 e, uint
     }
     return bits;
 }
+// LDS bytes of k_enc_xn's workgroup (ring | encode table | input tiles)
+template <uint32_t EW>
+constexpr uint32_t enc_xn_lds_bytes() {
+    return (ZR_ENC_DB != 0 ? 16u : 32u) * EW * 4 + 256u * 16 * (EW == 1024 ? 16u : 1u) + (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
+}
+// the encoder of workgroup vblk (its blockIdx.x in k_enc_xn; k_enc_cmp_fused
+// runs it beside the compaction of other buffers), LDS from the caller
 template <uint32_t EW, int ABL, bool IL>
-__global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
+__device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, const RansWork &w, uint32_t vblk,
+                                            uint8_t *const lds) {
     // DB: two input tiles, written alternately, so one barrier per tile
     // separates a tile's writes from its reads (the other barrier kept the
     // next tile's writes from overtaking slow readers); the room comes from a
@@ -588,7 +603,7 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // round trip on the wave: encoder 0.164 -> 0.173 ms, record encoder
     // 0.675 -> 0.688 ms. Dropped.)
     constexpr uint32_t RING_ALLOC = RING_BYTES;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[RING_ALLOC + 256 * 16 * TC + (DB ? 2 : 1) * ETILE * EW];
+    static_assert(enc_xn_lds_bytes<EW>() == RING_ALLOC + 256 * 16 * TC + (DB ? 2 : 1) * ETILE * EW, "LDS layout");
     uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
     uint4 *et = reinterpret_cast<uint4 *>(lds + RING_ALLOC);
     uint8_t *itile = lds + RING_ALLOC + 256 * 16 * TC;
@@ -602,9 +617,9 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     // to workgroups on the same XCD (workgroups are dealt to the 8 XCDs round
     // robin), so the line is fetched into one L2 once, not into two (the grid is
     // padded to a multiple of 16)
-    uint32_t lin = blockIdx.x;
+    uint32_t lin = vblk;
     if (EW == 64) {
-        const uint32_t g = blockIdx.x / 16, r = blockIdx.x % 16;
+        const uint32_t g = vblk / 16, r = vblk % 16;
         lin = 2 * (g * 8 + (r % 8)) + r / 8;
     }
     const uint32_t b = lin / nblkE, blk = lin % nblkE;
@@ -1009,6 +1024,12 @@ __global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, Rans
     }
 }
 
+template <uint32_t EW, int ABL, bool IL>
+__global__ __launch_bounds__(EW) void k_enc_xn(const uint8_t *raw, KArgs a, RansWork w) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[enc_xn_lds_bytes<EW>()];
+    enc_xn_body<EW, ABL, IL>(raw, a, w, blockIdx.x, lds);
+}
+
 // ======================================================================
 // encode/decode, x1 layout: one lane per buffer (encode_single rans.rs:354-366)
 // ======================================================================
@@ -1113,15 +1134,34 @@ __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, Ra
 // in the window are skipped lanes.
 // ABL (ZR_DIAG builds, profiling only): 1 no phase-2 global stores, 2 no phase-1
 // LDS image writes, 4 phase-1 loads all read the group's first 256 B
+// the compaction's LDS (one struct, so that k_enc_cmp_fused can lay it over
+// the encoder's)
+template <uint32_t CS, uint32_t CWIN>
+struct CmpLds {
+    unsigned long long sh[4];
+    uint64_t soff[CS];
+    uint32_t slen[CS], cpre[CS + 1], clo[CS], crng[2], sfail;
+    int ilm[CS][4];  // IL, per stream in the window: quad rows [x, y), image bytes [z, w) (z: its quad 0)
+    __attribute__((aligned(16))) uint8_t img[CWIN];
+};
 template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0>  // streams per group (divides 64), window bytes, loads in flight
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_lds(
-    uint8_t *enc, KArgs a, RansWork w, uint32_t nwin, int has_off) {
+__device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const RansWork &w, uint32_t nwin,
+                                             int has_off, uint32_t vblk, uint8_t *const smem) {
     static_assert(CS <= 64 && 64 % CS == 0, "a group's streams are lanes of one wave");
+    CmpLds<CS, CWIN> &S = *reinterpret_cast<CmpLds<CS, CWIN> *>(smem);
+    auto &sh = S.sh;
+    auto &soff = S.soff;
+    auto &slen = S.slen;
+    auto &cpre = S.cpre;
+    auto &clo = S.clo;
+    auto &crng = S.crng;
+    int4 *const ilm = reinterpret_cast<int4 *>(&S.ilm[0][0]);
+    auto &img = S.img;
     const uint32_t nblk = w.nblk;
     const uint32_t gpb = 256 / CS;  // groups per 256-stream block
     const uint32_t ngrp = nblk * gpb;
-    const uint32_t wi = blockIdx.x % nwin;
-    const uint32_t gid = blockIdx.x / nwin;
+    const uint32_t wi = vblk % nwin;
+    const uint32_t gid = vblk / nwin;
     const uint32_t b = gid / ngrp, grp = gid % ngrp;
     if (b >= a.B) return;
     const uint64_t n = a.len[b];
@@ -1130,11 +1170,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     const uint32_t blk = grp / gpb, s0 = grp * CS;
     if (s0 >= N) return;
     const uint32_t ns = min(CS, N - s0);
-    __shared__ unsigned long long sh[4];
-    __shared__ uint64_t soff[CS];
-    __shared__ uint32_t slen[CS], cpre[CS + 1], clo[CS], crng[2];
-    __shared__ int4 ilm[CS];  // IL, per stream in the window: quad rows [x, y), image bytes [z, w) (z: its quad 0)
-    __shared__ __attribute__((aligned(16))) uint8_t img[CWIN];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wv = tid >> 6;
     uint8_t *dbase = enc + a.enc_off[b] + 12 * (size_t)N;
@@ -1220,7 +1255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         // the encoder left every stream's offset in its block (st_off): wave 0
         // alone sums the <= 64 block sums below this block and sets the group
         // up, one barrier, no block scan
-        __shared__ uint32_t sfail;
+        uint32_t &sfail = S.sfail;
         if (wv == 0) {
             // every load of the setup issued at once (one memory round trip): the
             // block sums, and the group's lengths, offsets and (first window)
@@ -1446,6 +1481,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         }
         __syncthreads();
     }
+}
+
+template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_lds(
+    uint8_t *enc, KArgs a, RansWork w, uint32_t nwin, int has_off) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[sizeof(CmpLds<CS, CWIN>)];
+    compact_body<CS, CWIN, CU_LD, IL, ABL>(enc, a, w, nwin, has_off, blockIdx.x, smem);
+}
+
+// The second launch of a split encode (zr_rans_encode_batch_dev, SPLIT): the
+// encoder of the upper half of the buffers (workgroups [0, nenc), their KArgs
+// and RansWork rebased on that half) and the compaction of the lower half,
+// whose encoder ran in the launch before, in one dispatch. The encoder's
+// workgroups come first (the dispatcher places them first: 2 per CU at 2^18
+// streams); the compaction's fill the CU's remaining slots and move the lower
+// half's bytes while the upper half's chains run. One launch instead of two
+// streams: a cross-stream event costs the queue ~5 us.
+template <bool IL>
+__global__ __launch_bounds__(256) void k_enc_cmp_fused(const uint8_t *raw, uint8_t *enc, KArgs ahi, RansWork whi,
+                                                       uint32_t nenc, KArgs alo, RansWork wlo, int has_off) {
+    constexpr uint32_t CWIN = 19 * 1024;
+    constexpr uint32_t L = enc_xn_lds_bytes<256>() > sizeof(CmpLds<16, CWIN>) ? enc_xn_lds_bytes<256>()
+                                                                               : (uint32_t)sizeof(CmpLds<16, CWIN>);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[L];
+    if (blockIdx.x < nenc)
+        enc_xn_body<256, 0, IL>(raw, ahi, whi, blockIdx.x, lds);
+    else
+        compact_body<16, CWIN, 4, IL>(enc, alo, wlo, 1, has_off, blockIdx.x - nenc, lds);
 }
 
 // ======================================================================
@@ -3182,6 +3245,30 @@ static uint64_t next_epoch() {
 
 static bool narrow_batch(const KArgs &a) { return (uint64_t)a.B * a.N <= (1u << 16); }
 
+// buffers [b0, b0 + nb) of a batch as a batch of their own (kernels index
+// every per-buffer array by the buffer, so the bases move)
+static KArgs kargs_sub(const KArgs &a, uint32_t b0, uint32_t nb) {
+    KArgs r = a;
+    r.B = nb;
+    r.len += b0;
+    r.raw_off += b0;
+    r.enc_off += b0;
+    r.enc_len += b0;
+    r.status += b0;
+    r.tables = reinterpret_cast<const RansDTab *>(a.tables) + (size_t)a.table_stride * b0;
+    return r;
+}
+static RansWork work_sub(const RansWork &w, uint32_t N, uint32_t b0) {
+    RansWork r = w;
+    r.st_state += (size_t)b0 * N;
+    r.st_len += (size_t)b0 * N;
+    r.st_off += (size_t)b0 * N;
+    r.blocksum += (size_t)b0 * w.nblk;
+    r.blockoff += (size_t)b0 * w.nblk;
+    r.scratch += (size_t)b0 * w.region;
+    return r;
+}
+
 static KArgs kargs(const zr_rans_batch *bt) {
     KArgs a;
     a.B = bt->n_buffers;
@@ -3211,6 +3298,15 @@ int32_t zr_rans_set_encoder_width(uint32_t lanes) {
     g_enc_width.store(lanes, std::memory_order_relaxed);
     return ZR_OK;
 }
+
+int32_t zr_rans_set_encode_split(int32_t quarters) {
+    clear_error();
+    if (quarters < 0 || quarters > 3) return set_error(ZR_INVALID_INPUT, "encode split must be 0..3 quarters");
+    g_enc_split.store(quarters, std::memory_order_relaxed);
+    return ZR_OK;
+}
+
+int32_t zr_rans_get_encode_split(void) { return g_enc_split.load(std::memory_order_relaxed); }
 
 int32_t zr_rans_selftest_reciprocal(uint64_t *mismatches) {
     ZR_GUARD_BEGIN
@@ -3396,9 +3492,27 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         else if (wide)
             launch_timed("rans_encode", w.il ? k_enc_xn<1024, 0, true> : k_enc_xn<1024, 0, false>,
                          dim3((uint32_t)(a.N / 1024 * a.B)), dim3(1024), 0, s, raw, a, w);
-        else
+        // split (256-lane shape, one window per group, offsets from the
+        // encoder, halves of >= 2^17 streams): see g_enc_split
+        const uint32_t sq = (uint32_t)g_enc_split.load(std::memory_order_relaxed);  // the lower part, in quarters
+        const uint32_t hB = (uint32_t)(((uint64_t)a.B * sq + 2) / 4);
+        const bool split = sq && !narrow && !wide && hB >= 1 && hB < a.B && (uint64_t)a.B * a.N >= (1u << 18) &&
+                           w.nblk <= SCAN_FUSE && 256ull * w.cap < (1ull << 32) &&
+                           (16ull * w.cap + 16) / (19 * 1024) / 2 <= 1 && kenc == (w.il ? k_enc_xn<256, 0, true> : k_enc_xn<256, 0, false>);
+        if (split) {
+            const KArgs alo = kargs_sub(a, 0, hB), ahi = kargs_sub(a, hB, a.B - hB);
+            const RansWork wlo = work_sub(w, a.N, 0), whi = work_sub(w, a.N, hB);
+            const uint32_t nlo = hB * w.nblk, nhi = (a.B - hB) * w.nblk;  // encoder workgroups per half
+            launch_timed("rans_encode", kenc, dim3(nlo), dim3(256), 0, s, raw, alo, wlo);
+            launch_timed("rans_encode_compact", w.il ? k_enc_cmp_fused<true> : k_enc_cmp_fused<false>,
+                         dim3(nhi + 16 * nlo), dim3(256), 0, s, raw, enc, ahi, whi, nhi, alo, wlo, 1);
+            constexpr uint32_t CWIN = 19 * 1024;
+            launch_timed("rans_compact", w.il ? k_enc_compact_lds<16, CWIN, 4, true> : k_enc_compact_lds<16, CWIN, 4, false>,
+                         dim3(16 * nhi), dim3(256), 0, s, enc, ahi, whi, 1u, 1);
+        } else if (!narrow && !wide) {
             launch_timed("rans_encode", kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
-        {
+        }
+        if (!split) {
             if (w.nblk > SCAN_FUSE)  // (otherwise the compaction scans the block sums itself)
                 hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
             // 16 streams per group, 19 KiB windows (8 workgroups per CU), four 16-B loads in
