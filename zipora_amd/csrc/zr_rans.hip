@@ -2883,6 +2883,9 @@ __global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t
 constexpr uint32_t XF = 1024;  // records per workgroup
 constexpr uint32_t XG = 8;     // tiles per output group (16 * XG bytes per lane per store run)
 constexpr uint32_t NSET = 1;   // staging register sets: a refill lands NSET boundaries after its loads
+#ifndef ZR_X1_T32
+#define ZR_X1_T32 1  // 32-step tiles with the predicted-consumption refill rule
+#endif
 
 // taken[b] (workspace, one word per buffer): 1 for the records this kernel
 // decodes, 0 for the other x1 records (k_dec_x1_ring's), so that kernel need not
@@ -3088,10 +3091,119 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
     };
     const uint32_t nreg = cmin / (16 * XG);  // groups in which every fast lane of the wave is live
     uint32_t g = 0;
+    if constexpr (ZR_X1_T32) {
+        // ---- 32-step tiles (k_dec_xn_fast's wide-shape refill rule): a
+        // boundary every 32 steps instead of 16. A lane issues the segment
+        // below when it will have consumed its ring rows by the next boundary,
+        // predicting that the next tile consumes what the last one did; the
+        // segment lands there if those rows are consumed, else it is fetched
+        // again. Same groups of 128 steps (4 tiles) and 128-B stores.
+        constexpr uint32_t TT = 32, TPG = 16 * XG / TT;
+        const uint32_t nt32 = (cmax + TT - 1) / TT;
+        uint32_t ppos8 = pos8 + TT * 8;  // pos8 at the previous boundary (first: one byte a step)
+        auto boundary32 = [&](uint32_t t, auto wc) __attribute__((always_inline)) {
+            // every read of tile t - 1 (lanes live in it) was at or above pos - 4
+            bad |= fast && TT * t < nn + TT && (int32_t)(pos8 - 32 - ((uint32_t)lo64 << 3)) < 0;
+            if (t >= 1) {
+                asm volatile("s_waitcnt vmcnt(%4)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3) : "i"(decltype(wc)::value) : "memory");
+                const bool landable = (int32_t)(pos8 - ((uint32_t)lo64 << 3)) <= 64 * 8;
+                if (pnd && landable) {
+                    lo64 -= 64;
+                    put_seg((uint32_t)lo64, e0, e1, e2, e3);
+                }
+                pnd = pnd && !landable;
+            }
+            const uint32_t used8 = ppos8 - pos8;
+            ppos8 = pos8;
+            const bool need = fast && TT * t < nn && (int32_t)(pos8 - used8 - ((uint32_t)lo64 << 3)) <= 64 * 8;
+            const bool issue = pnd || need;  // (a segment that did not land: fetched again)
+            const uintptr_t ga = issue ? clampa(lo64 - 64) : dummy;
+            asm_load16(e0, ga);
+            asm_load16_off<16>(e1, ga);
+            asm_load16_off<32>(e2, ga);
+            asm_load16_off<48>(e3, ga);
+            pnd = issue;
+        };
+        auto tile32 = [&](uint32_t t, uint32_t *o, auto irr) __attribute__((always_inline)) {
+            uint32_t D = readD(pos8);
+            uint32_t lo2 = 0;
+#pragma unroll
+            for (int j = 0; j < (int)TT / 2; j++) {
+                uint32_t hA, lA, sA, hB, lB, sB;
+                const uint32_t eA = step(D, hA, lA, sA);
+                const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
+                uint32_t used;
+                asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
+                if constexpr (decltype(irr)::value) {
+                    const uint32_t kA = TT * t + 2 * j;
+                    pos_snap = kA < nn ? pos8 + 8 - sA : pos_snap;
+                    pos_snap = kA + 1 < nn ? pos8 - used : pos_snap;
+                }
+                pos8 -= used;
+                if (j + 1 < (int)TT / 2) D = readD(pos8);
+                uint32_t pr = __builtin_amdgcn_perm(eB, eA, 0x0c0c0400u);
+                asm volatile("" : "+v"(pr));
+                if (j & 1)
+                    o[j >> 1] = __builtin_amdgcn_perm(pr, lo2, 0x05040100u);
+                else
+                    lo2 = pr;
+            }
+            if constexpr (!decltype(irr)::value) pos_snap = pos8;
+        };
+        using W0 = std::integral_constant<int, 0>;
+        using WX = std::integral_constant<int, XG>;
+        auto resync = [&]() __attribute__((always_inline)) {
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
+        };
+        auto group32 = [&](uint32_t g, auto irr) __attribute__((always_inline)) {
+            constexpr bool IRR = decltype(irr)::value;
+            uint32_t o[4 * XG];
+            const uint32_t t0 = TPG * g;
+            boundary32(t0, WX());  // (younger than the last boundary's loads: the previous group's stores)
+            tile32(t0, o, irr);
+#pragma unroll
+            for (uint32_t k = 1; k < TPG; k++) {
+                if (!IRR || t0 + k < nt32) {
+                    boundary32(t0 + k, W0());
+                    tile32(t0 + k, o + (TT / 4) * k, irr);
+                }
+            }
+            x4u *d = reinterpret_cast<x4u *>(out + 16 * XG * (size_t)g);
+            if constexpr (!IRR) {
+                if (fast) {
+#pragma unroll
+                    for (uint32_t k = 0; k < XG; k++) d[k] = x4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                }
+            } else {
+                if (fast && nn > 16 * XG * g) {
+                    const uint32_t full = min(nn - 16 * XG * g, 16 * XG);
+                    if (full == 16 * XG) {
+#pragma unroll
+                        for (uint32_t k = 0; k < XG; k++) d[k] = x4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                    } else {
+                        uint8_t *db = reinterpret_cast<uint8_t *>(d);
+                        uint32_t wl = 0;
+#pragma unroll
+                        for (uint32_t k = 0; k < 4 * XG; k++) {
+                            if (4 * k + 4 <= full) *reinterpret_cast<uint32_t *>(db + 4 * k) = o[k];
+                            wl = k == (full >> 2) ? o[k] : wl;
+                        }
+                        for (uint32_t i = full & ~3u; i < full; i++) db[i] = (uint8_t)(wl >> (8 * (i & 3)));
+                    }
+                }
+                resync();  // per-lane stores: resynchronise the vmcnt accounting
+            }
+        };
+        const uint32_t ng32 = (nt32 + TPG - 1) / TPG;
+        for (; g < nreg; g++) group32(g, std::false_type());
+        for (; g < ng32; g++) group32(g, std::true_type());
+        bad |= fast && TT * (nt32 - 1) < nn && (int32_t)(pos8 - 32 - ((uint32_t)lo64 << 3)) < 0;
+    } else {
     for (; g < nreg; g++) group(g, std::false_type());
     for (; g < ngrp; g++) group(g, std::true_type());
     // the reads of the wave's last tile (lanes live in it)
     bad |= fast && 16 * (ntile - 1) < nn && (int32_t)(pos8 - 32 - ((uint32_t)lo64 << 3)) < 0;
+    }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1), "+v"(f2),
                  "+v"(f3)::"memory");
     if (fast) {
