@@ -252,7 +252,7 @@ def test_rans_host_pipe_packed(zr, oracle):
 
 
 def test_rans_host_pipe(zr, oracle):
-    # several groups per call (both slots reused), a buffer larger than a group,
+    # several groups per call (every device slot reused), a buffer larger than a group,
     # empty and tiny buffers, pageable memory
     lens = [300000, 0, 5, 70000, 1 << 20, 4096, 200000, 123457, 1, 90000]
     _pipe_roundtrip(zr, oracle, lens, 4096, "u", 256 << 10)

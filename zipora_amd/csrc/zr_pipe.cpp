@@ -3,9 +3,9 @@
 // host memory).
 //
 // The buffers of a call are cut into groups of whole buffers (contiguous in
-// host memory). Each group goes through one of two device slots on three HIP
-// streams, so group g+1's host-to-device copy, group g's coding and group
-// g-1's device-to-host copy run at the same time:
+// host memory). Each group goes through one of ZR_PIPE_SLOTS (3) device slots
+// on three HIP streams, so group g+1's host-to-device copy, group g's coding
+// and group g-1's device-to-host copy run at the same time:
 //
 //   s_in : input span H2D -> event in_done
 //   s_cmp: wait in_done, meta in, zr_rans_{encode,decode}_batch_dev, lengths and
@@ -109,11 +109,21 @@ int32_t copy_words(const uint64_t *src, uint64_t *dst, size_t n, hipStream_t s) 
 
 }  // namespace
 
+// device slots: a group's input copy waits for the copy back of the group
+// ZR_PIPE_SLOTS earlier (the slot it reuses). With two, group g+1's input copy
+// waited for group g-1's copy back, which waits for group g-1's coding: the
+// input link idled for a coding time per group. Same box, 64 x 4 MiB x4096,
+// pinned (tools/pipe_ab.py): encode 26-27.5 -> 36-37 GiB/s, decode 37 -> 39.5,
+// both 15.5 -> 19.0; 1 M x 1 KiB records 16.4 -> 19.2; four slots: the same
+// as three.
+#ifndef ZR_PIPE_SLOTS
+#define ZR_PIPE_SLOTS 3
+#endif
 struct zr_rans_pipe {
     uint32_t N = 1;
     uint64_t group_cap = 0;
     hipStream_t s_in = nullptr, s_cmp = nullptr, s_out = nullptr;
-    Slot slot[2];
+    Slot slot[ZR_PIPE_SLOTS];
     void *dtab = nullptr;  // the shared device table
 };
 
@@ -267,7 +277,7 @@ int32_t run_impl(zr_rans_pipe *p, bool encode, uint32_t B, const uint64_t *len, 
     std::vector<uint8_t> use_pack(gs.size(), 0);  // packed groups of small records: device packing
 
     auto issue_out = [&](size_t gi) -> int32_t {
-        Slot &S = p->slot[gi & 1];
+        Slot &S = p->slot[gi % ZR_PIPE_SLOTS];
         const uint32_t b0 = gs[gi].first, b1 = gs[gi].second, nb = b1 - b0;
         ZR_HIP(hipStreamWaitEvent(p->s_out, S.code_done, 0));
         tr.mark(gi, 4, p->s_out);
@@ -312,7 +322,7 @@ int32_t run_impl(zr_rans_pipe *p, bool encode, uint32_t B, const uint64_t *len, 
     };
 
     for (size_t gi = 0; gi < gs.size(); gi++) {
-        Slot &S = p->slot[gi & 1];
+        Slot &S = p->slot[gi % ZR_PIPE_SLOTS];
         if (S.busy) {  // the slot's previous group: wait for its copies back, keep its results
             ZR_HIP(hipEventSynchronize(S.out_done));
             collect(S, encode ? enc_len : nullptr, status);
