@@ -55,11 +55,12 @@ def test_x1_whole_groups_many_workgroups(zr, oracle, kind):
 
 @pytest.mark.parametrize("N", [1, 4096])
 def test_x1_ragged_records(zr, oracle, N):
-    # lengths around every tile (16), group (64) and line (128) boundary, random
-    # ones, empty records; with N = 4096 the records >= 4096 take the xN layout
+    # lengths around every tile (16 and, since round 4, 32 steps), group (64),
+    # line and output group (128) boundary, random ones, empty records; with
+    # N = 4096 the records >= 4096 take the xN layout
     rnd = random.Random(11 + N)
-    edge = [0, 1, 2, 7, 8, 15, 16, 17, 31, 32, 63, 64, 65, 127, 128, 129, 191, 192, 255, 256, 257,
-            1000, 1023, 1024, 1025, 4095, 4096, 5000, 20000]
+    edge = [0, 1, 2, 7, 8, 15, 16, 17, 31, 32, 33, 63, 64, 65, 95, 96, 97, 127, 128, 129, 159, 160, 161,
+            191, 192, 193, 255, 256, 257, 1000, 1023, 1024, 1025, 4095, 4096, 5000, 20000]
     lens = edge * 8 + [rnd.randrange(0, 3000) for _ in range(1800)]
     rnd.shuffle(lens)
     datas = [zr.synth("t", n, seed=100 + b) for b, n in enumerate(lens)]
