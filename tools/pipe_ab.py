@@ -1,6 +1,7 @@
 """Host pipeline (zr_rans_pipe_*) encode / decode rates of the library named by
-ZR_LIB_PATH, pinned host areas, two shapes: 64 x 4 MiB x4096 (the headline's)
+ZR_LIB_PATH (groups of $GROUP_MIB MiB, default 32), pinned host areas, two shapes: 64 x 4 MiB x4096 (the headline's)
 and 1 M x 1 KiB records x1 (configs[4]). Prints one line per shape."""
+import os
 import sys
 import time
 
@@ -17,7 +18,7 @@ def rates(lens, N, kind, reps=3):
     total = int(lens.sum())
     host = zr.synth(kind, total, seed=7)
     hist = [int(v) for v in np.bincount(np.frombuffer(host, dtype=np.uint8), minlength=256)]
-    pipe = RansHostPipe(zr.Rans64Encoder(hist, N).table, N)
+    pipe = RansHostPipe(zr.Rans64Encoder(hist, N).table, N, int(os.environ.get("GROUP_MIB", "32")) << 20)
     raw_off, _, rb, eb = pipe.layout(lens)
     pin = torch.empty(rb, dtype=torch.uint8, pin_memory=True)
     pin.copy_(torch.frombuffer(bytearray(host), dtype=torch.uint8))
