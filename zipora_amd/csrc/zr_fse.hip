@@ -735,6 +735,9 @@ __device__ __forceinline__ void fse_asm_load16(fv4u &dst, const fv4u *p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
 }
 
+#ifndef ZR_FSE_PK
+#define ZR_FSE_PK 1
+#endif
 // Fast path for blocks coded with block 0's table (every block of a stream
 // this library or the reference wrote from one histogram). Per lane: a
 // 64-dword LDS ring of the word area indexed by absolute dword index mod 64
@@ -831,7 +834,7 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
         const uint64_t merged = ((uint64_t)xl << 32) | max(w, __builtin_elementwise_sub_sat(1u, xl));
         x = small ? merged : xd;
         m32 -= small ? 1 : 0;
-        return e & 0xFF;
+        return e;  // (the symbol is the low byte; the caller packs)
     };
     const uint32_t G = fast ? (uint32_t)(B.orig >> 4) : 0u;
     const bool vec = (((uintptr_t)out) & 15) == 0;
@@ -868,8 +871,21 @@ __global__ __launch_bounds__(64) void k_fse_dec(FseDecArgs a) {
             uint32_t o[4] = {0, 0, 0, 0};
             if (bp >= 68) {
                 uint32_t m32 = (uint32_t)m;
+                if (ZR_FSE_PK) {
+                    // the step returns the slot entry e (symbol in its low
+                    // byte); four symbols pack into a dword with two v_perm
+                    // and an or instead of a mask and a shift-or each
 #pragma unroll
-                for (int k = 0; k < 16; k++) o[k >> 2] |= step_bulk(m32) << (8 * (k & 3));
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t e0 = step_bulk(m32), e1 = step_bulk(m32);
+                        const uint32_t lo = __builtin_amdgcn_perm(e1, e0, 0x0c0c0400u);  // [e0, e1, 0, 0]
+                        const uint32_t e2 = step_bulk(m32), e3 = step_bulk(m32);
+                        o[q] = __builtin_amdgcn_perm(e3, e2, 0x04000c0cu) | lo;  // [.., .., e2, e3]
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 16; k++) o[k >> 2] |= (step_bulk(m32) & 0xFF) << (8 * (k & 3));
+                }
                 const uint32_t used = (uint32_t)m - m32;  // words merged by the group
                 m -= used;
                 bp -= 4ull * used;
