@@ -838,8 +838,9 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     if diag:  # tools/*.sh read the kernel times; no metric from a diagnostic build
         return {"diagnostic": diag, "kernels_ms": kms, "ms_per_step": round(dt / args.steps * 1e3, 4),
                 "timed_ms": {k: round(v, 4) for k, v in tms.items()}}
-    literal = B == 1
-    wl = "rans_literal" if literal else "rans"
+    single = B == 1
+    literal = single and N == 4096
+    wl = "rans_literal" if literal else f"rans_n2e{N.bit_length() - 1}" if single else "rans"
     rans_bytes = {"rans_encode": total + comp_bytes, "rans_decode": comp_bytes + total,
                   "rans_compact": 2 * comp_bytes, "histogram": total}
     if split:
@@ -867,6 +868,10 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
         "config": {"workload": (f"BASELINE configs[1] as written: rANS O0 encode+decode of ONE {n >> 20} MiB "
                                 f"uniform buffer per GPU, {N}-way interleaved streams ({n // N} symbols per stream)"
                                 if literal else
+                                f"BASELINE.md C2 at N = {N}: rANS O0 encode+decode of ONE {n >> 20} MiB uniform "
+                                f"buffer per GPU, {N}-way interleaved streams ({n // N} symbols per stream; the "
+                                f"reference takes any N, rans.rs:165-168)"
+                                if single else
                                 f"rANS O0 encode+decode, {total >> 20} MiB uniform bytes per GPU as "
                                 f"{B} x {n >> 20} MiB buffers, {N}-way interleaved streams each "
                                 f"({B * N} streams), shared table (histogram all-reduce over ranks)"),
@@ -894,7 +899,7 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     if rank == 0 and world == 1 and cpu and not args.no_cpu_baseline:
         # literal config: 16 MiB slices of the buffer, each its own x4096 stream set
         res["cpu_baseline"] = cpu_baseline(host, n, B, N, cpu_threads(args),
-                                           sample_bytes=(16 << 20) if literal else None)
+                                           sample_bytes=(16 << 20) if single else None)
     del raw, enc, out, bt
     return res
 
@@ -926,6 +931,10 @@ def secondary_lines(args, torch, dist, world, rank, dev, zr, L, host):
     out["rans_literal"] = slim(run_rans(sub(3, 1), torch, dist, world, rank, dev, zr, L, 1, 256 << 20, 4096,
                                         host=host, host_path=False))
     torch.cuda.empty_cache()
+    # BASELINE.md C2's other stream count, N = 2^18, on ONE 256 MiB buffer
+    out["rans_n2e18"] = slim(run_rans(sub(5, 2), torch, dist, world, rank, dev, zr, L, 1, 256 << 20, 1 << 18,
+                                      host=host, host_path=False))
+    torch.cuda.empty_cache()
     a = sub(3, 1)
     a.fse_block_kib = 64
     out["fse"] = slim(run_fse(a, torch, dist, world, rank, dev, zr, L))
@@ -954,25 +963,55 @@ def launch(args):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    # (the port is free when probed; a process that takes it before rank 0
+    # binds it makes rank 0's rendezvous fail, and the launch exits non-zero)
+    import signal
+
+    class _Stop(Exception):
+        pass
+
+    def _on_signal(signum, frame):
+        raise _Stop(signum)
+
+    old = {sig: signal.signal(sig, _on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc, alive = 0, set(range(n))
-    while alive:
-        for i in sorted(alive):
-            c = procs[i].poll()
-            if c is None:
-                continue
-            alive.discard(i)
-            if c != 0 and rc == 0:
-                rc = c if c > 0 else 128 - c
-                print(f"bench.py: rank {i} exited with {c}; stopping the other ranks", file=sys.stderr)
-                for j in alive:
-                    procs[j].terminate()
-        time.sleep(0.1)
+    rc, alive = 0, set()
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+            alive.add(r)
+        while alive:
+            for i in sorted(alive):
+                c = procs[i].poll()
+                if c is None:
+                    continue
+                alive.discard(i)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print(f"bench.py: rank {i} exited with {c}; stopping the other ranks", file=sys.stderr)
+                    for j in alive:
+                        procs[j].terminate()
+            time.sleep(0.1)
+    except _Stop as e:
+        print(f"bench.py: signal {e.args[0]}; stopping the ranks", file=sys.stderr)
+        rc = 128 + int(e.args[0])
+    finally:
+        # no rank outlives the launcher (a killed parent would leave them holding GPUs)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        for sig, h in old.items():
+            signal.signal(sig, h)
     return rc
 
 

@@ -162,7 +162,11 @@ int32_t zr_rans_dtab_from_hist_consume_dev(uint32_t *hist_dev, uint32_t n_tables
  * (blob_store/entropy.rs:212-222, compression/mod.rs:433-450). hist_dev: 256
  * u32, all zero on entry, left all zero (the counts are consumed). Not on a
  * capturing stream (ZR_UNSUPPORTED): each call picks its workgroups' ticket
- * counters by a host-side call counter. */
+ * counters by a host-side call counter, slot (call number % 64). Limit: fewer
+ * than 64 calls of this function may be executing at once in the process
+ * (calls queued on one stream run one after another and never share a slot;
+ * 64 or more concurrent streams each running one could pair two calls on a
+ * slot, and a table would then be built before its histogram is complete). */
 int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *batch, uint32_t *hist_dev,
                                    void *dtab_dev, void *stream);
 /* Tuning (no reference counterpart): the workgroup width of the xN encoder for

@@ -649,6 +649,24 @@ int or_fse_compress_freqs(const or_fse_config *c, const uint32_t *freqs, const u
     return st;
 }
 
+/* FseTable::renormalize_decode, fse.rs:704-735: after a decoded symbol, while
+   fewer than 4 bytes are left one byte is read, else one u32 LE word; the
+   state never drops below 1. (The reference's `pos + 4 <= len` guard always
+   holds once pos >= 4, so the word is always read.) Returns the new state. */
+uint64_t or_fse_renormalize_decode(uint64_t x, const uint8_t *in, size_t len, size_t *pos) {
+    (void)len;
+    if (x < 65536 && *pos > 0) {
+        if (*pos >= 4) {
+            *pos -= 4;
+            x = (x << 32) | rd_u32(in + *pos);
+        } else {
+            *pos -= 1;
+            x = (x << 8) | in[*pos];
+        }
+    }
+    return x < 1 ? 1 : x;
+}
+
 /* decompress_single, fse.rs:1151-1281. Appends to o. */
 static int fse_decompress_single(const uint8_t *data, size_t len, bvec *o, size_t out_cap) {
     if (len == 0) return OK;
@@ -701,17 +719,7 @@ static int fse_decompress_single(const uint8_t *data, size_t len, bvec *o, size_
         uint8_t s = t->alias[lo];
         x = (uint64_t)t->dfreq[s] * (x >> 12) + lo - t->dstart[s];
         o->p[o->n++] = s;
-        /* renormalize_decode, fse.rs:704-735 */
-        if (x < 65536 && bp > 0) {
-            if (bp >= 4) {
-                bp -= 4;
-                x = (x << 32) | rd_u32(cd + bp);
-            } else {
-                bp -= 1;
-                x = (x << 8) | cd[bp];
-            }
-        }
-        if (x < 1) x = 1;
+        x = or_fse_renormalize_decode(x, cd, state_start - pos, &bp);
     }
     free(t);
     return OK;

@@ -66,6 +66,8 @@ def lib():
         L.or_fse_decompressed_size.argtypes = [u8p, sz, ctypes.POINTER(sz)]
         L.or_fse_mul_hi.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         L.or_fse_mul_hi.restype = ctypes.c_uint64
+        L.or_fse_renormalize_decode.argtypes = [ctypes.c_uint64, u8p, sz, ctypes.POINTER(sz)]
+        L.or_fse_renormalize_decode.restype = ctypes.c_uint64
         L.or_fse_normalize_exact.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32,
                                              ctypes.POINTER(ctypes.c_uint32)]
         L.or_huff_tree_build.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(HuffTree)]
@@ -222,6 +224,14 @@ def fse_compress_freqs(data, freqs, config=None):
     _check(lib().or_fse_compress_freqs(ctypes.byref(c), (ctypes.c_uint32 * 256)(*freqs), b, n, out,
                                        ctypes.byref(ol)), "fse_compress_freqs")
     return ctypes.string_at(out, ol.value)
+
+
+def fse_renormalize_decode(state, data, pos):
+    """FseTable::renormalize_decode (fse.rs:704-735): returns (state, pos)."""
+    p = sz(pos)
+    b, n = _buf(data)
+    x = lib().or_fse_renormalize_decode(state, b, n, ctypes.byref(p))
+    return x, p.value
 
 
 def fse_decompress(data, cap=None):

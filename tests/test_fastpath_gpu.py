@@ -37,9 +37,14 @@ def _batch_roundtrip(zr, oracle, lens, N, kind, seed, check_bufs=2, skew=False):
     fb = zr.fallback_lanes(reset=True)
     assert torch.equal(out, raw)
     if check_bufs:
+        import concurrent.futures as cf
         t = oracle.rans_table(oracle.histogram(b"".join(datas)))
-        for b in range(min(check_bufs, len(lens))):
-            assert bt.encoded(enc, b) == oracle.rans_encode(t, N, datas[b]), f"buffer {b}"
+        nb = min(check_bufs, len(lens))
+        # (the oracle releases the GIL: the buffers are encoded on 16 threads)
+        with cf.ThreadPoolExecutor(max_workers=16) as ex:
+            refs = list(ex.map(lambda b: oracle.rans_encode(t, N, datas[b]), range(nb)))
+        for b in range(nb):
+            assert bt.encoded(enc, b) == refs[b], f"buffer {b}"
     return fb
 
 
@@ -47,7 +52,9 @@ def _batch_roundtrip(zr, oracle, lens, N, kind, seed, check_bufs=2, skew=False):
 def test_headline_shape_takes_fast_path(zr, oracle, kind):
     """64 x 4 MiB x 4096 streams (the bench's workload, 1024-lane decoder):
     uniform, Zipf(1.1) and text-like bytes decode with no generic lanes."""
-    fb = _batch_roundtrip(zr, oracle, [4 << 20] * 64, 4096, kind, 0x51 + ord(kind))
+    # every buffer of the uniform batch (the bench's input kind) byte-compared
+    fb = _batch_roundtrip(zr, oracle, [4 << 20] * 64, 4096, kind, 0x51 + ord(kind),
+                          check_bufs=64 if kind == "u" else 2)
     assert fb == 0, f"{fb} of {64 * 4096} streams fell back to the generic decoder ({kind})"
 
 
@@ -105,3 +112,14 @@ def test_record_batch_full_size(zr, oracle):
     fb = zr.fallback_lanes(reset=True)
     assert torch.equal(out, raw)
     assert fb == 0, f"{fb} of {R} records fell back to the generic decoder"
+
+
+@pytest.mark.parametrize("N", [1 << 18])
+def test_single_buffer_many_streams(zr, oracle, N):
+    """BASELINE.md C2 / SURVEY.md section 7 minimum slice: ONE 256 MiB uniform
+    buffer at N = 2^18 interleaved streams (1024 symbols per stream; the
+    reference takes any N, rans.rs:165-168): the whole encoded buffer
+    byte-compared with the oracle's encode_parallel (rans.rs:369-420), decoded
+    back with no generic lanes."""
+    fb = _batch_roundtrip(zr, oracle, [256 << 20], N, "u", 0x2E18, check_bufs=1)
+    assert fb == 0, f"{fb} of {N} streams fell back"

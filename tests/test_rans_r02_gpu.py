@@ -669,3 +669,79 @@ def test_table_from_data_fused(zr, oracle, kind, B, n):
         bt.raise_on_error()
         for b in range(min(B, 3)):
             assert bt.encoded(enc, b) == oracle.rans_encode(t, 4096, datas[b])
+
+
+@pytest.mark.parametrize("N,B,n,first_bad", [
+    (4096, 8, 8 * 4096, 3584),     # one-wave shape: 64 workgroups per buffer, last set = workgroups 56..63
+    (12288, 8, 6 * 12288, 8192),   # 1024-lane shape: 12 workgroups per buffer, last set = workgroups 8..11
+])
+def test_decode_errors_two_level_arrival(zr, oracle, N, B, n, first_bad):
+    """a buffer of more than DA_SET = 8 decoder workgroups
+    reports in two levels (sets of 8 on their own arrival words, the last of
+    each set on the buffer's word), so an error bit must pass through a set
+    word. Corruptions the oracle decides (truncation, moved lengths, a state
+    below 2^16) placed only in streams of the LAST set's workgroups; the status
+    must equal the oracle's, then a clean call on the same workspace reports OK
+    and decodes, then the corrupted call errs again (rans.rs:480-482, :601-610)."""
+    import torch
+    from zipora_amd.device import RansDeviceBatch
+    datas = [zr.synth("u" if b % 2 else "t", n, seed=5100 + b) for b in range(B)]
+    bt = RansDeviceBatch([n] * B, N, shared_table=False)
+    raw = _fill(bt, datas)
+    enc = bt.new_enc()
+    bt.full_encode(raw, enc)
+    torch.cuda.synchronize()
+    bt.raise_on_error()
+    tabs = [oracle.rans_table(oracle.histogram(d)) for d in datas]
+    clean = bytearray(enc.cpu().numpy().tobytes())
+    clean_len = bt.enc_len.cpu().tolist()
+    host, enc_len = bytearray(clean), list(clean_len)
+    rnd = random.Random(N)
+
+    def u32(buf, o):
+        return int.from_bytes(buf[o:o + 4], "little")
+
+    for b in range(1, B):  # buffer 0 stays clean: both statuses in one call
+        o, L = bt.enc_off_host[b], enc_len[b]
+        k = b % 3
+        if k == 0:  # truncated: the last streams run out of bytes
+            enc_len[b] = L - rnd.randrange(1, 8)
+        elif k == 1:  # 5 bytes moved between two streams of the last set
+            s = rnd.randrange(first_bad, N - 1)
+            ls, ls1 = o + 8 * N + 4 * s, o + 8 * N + 4 * (s + 1)
+            host[ls:ls + 4] = (u32(host, ls) - 5).to_bytes(4, "little")
+            host[ls1:ls1 + 4] = (u32(host, ls1) + 5).to_bytes(4, "little")
+        else:  # a state of the last set below 2^16
+            s = rnd.randrange(first_bad, N)
+            host[o + 8 * s:o + 8 * s + 8] = rnd.randrange(1, 1 << 16).to_bytes(8, "little")
+
+    def run(buf, lens):
+        enc.copy_(torch.frombuffer(bytes(buf), dtype=torch.uint8).cuda())
+        bt.enc_len.copy_(torch.tensor(lens, dtype=torch.int64))
+        bt.status.fill_(-3)
+        out = bt.new_raw()
+        bt.decode(enc, out)
+        torch.cuda.synchronize()
+        return bt.statuses(), out
+
+    def check(st, out, buf, lens):
+        n_err = 0
+        for b in range(B):
+            o = bt.enc_off_host[b]
+            try:
+                ref = oracle.rans_decode(tabs[b], N, bytes(buf[o:o + lens[b]]), n)
+            except oracle.OracleError:
+                ref = None
+            if ref is None:
+                n_err += 1
+                assert st[b] != 0, f"buffer {b}: the oracle errs, the GPU reports ok"
+            else:
+                assert st[b] == 0, f"buffer {b}: the oracle decodes, GPU status {st[b]}"
+                assert bt.raw_of(out, b) == ref, f"buffer {b}"
+        return n_err
+
+    assert check(*run(host, enc_len), host, enc_len) >= 3
+    st, out = run(clean, clean_len)
+    assert all(v == 0 for v in st)
+    assert check(st, out, clean, clean_len) == 0
+    assert check(*run(host, enc_len), host, enc_len) >= 3

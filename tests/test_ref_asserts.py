@@ -259,3 +259,78 @@ def test_fast_division_7():
         q = i if d <= 1 else (i * m) >> (32 + sh)  # divide (fse.rs:81-87)
         assert q == i // 7
         assert i - q * d == i % 7  # modulo (fse.rs:90-93)
+
+
+# --------------------------------------------------------------------------
+# fse.rs:1612-1618 and fse.rs:1621-1635: the FSE decoder's tail
+# --------------------------------------------------------------------------
+def test_fse_truncated_input_decoding_oracle(oracle):
+    """fse.rs:1612-1618: FseDecoder::new().decompress(&[0u8; 3]) is an error
+    (mode byte 0x00 is neither 0xF5 nor 0xF6)."""
+    with pytest.raises(oracle.OracleError):
+        oracle.fse_decompress(bytes(3))
+
+
+@gpu
+def test_fse_truncated_input_decoding():
+    """fse.rs:1612-1618 through the C ABI."""
+    with pytest.raises(zr.ZiporaError):
+        zr.fse_decompress(bytes(3))
+
+
+def test_fse_renormalize_decode_single_byte_steps(oracle):
+    """fse.rs:1621-1635: with 2 bytes left (< BLOCK_SIZE = 4) renormalize_decode
+    of state 100 reads one byte: Some(_), pos 2 -> 1. The state is then
+    (100 << 8) | input[1] (fse.rs:726-729)."""
+    x, pos = oracle.fse_renormalize_decode(100, bytes([0x12, 0x34]), 2)
+    assert pos == 1
+    assert x == (100 << 8) | 0x34
+    # and the other branches of fse.rs:712-733: a word read, no read at pos 0,
+    # no read at x >= 2^16, the max(x, 1) floor
+    x, pos = oracle.fse_renormalize_decode(100, bytes([1, 2, 3, 4, 5]), 5)
+    assert (x, pos) == ((100 << 32) | 0x05040302, 1)
+    assert oracle.fse_renormalize_decode(100, bytes([7]), 0) == (100, 0)
+    assert oracle.fse_renormalize_decode(1 << 16, bytes([7, 8]), 2) == (1 << 16, 2)
+    assert oracle.fse_renormalize_decode(0, b"", 0) == (1, 0)
+
+
+def _f5_with_word_area(words, state, orig_len, nsym=256):
+    """A crafted 0xF5 stream (fse.rs:887-966 layout): F5 | len u32 | 12 |
+    nsym u16 | (sym u8, freq u32) x nsym | word area | state u64, with the
+    uniform normalised table (4096 / nsym per symbol) and the given word area."""
+    import struct
+    f = 4096 // nsym
+    hdr = bytes([0xF5]) + struct.pack("<IBH", orig_len, 12, nsym)
+    tab = b"".join(struct.pack("<BI", s, f) for s in range(nsym))
+    return hdr + tab + bytes(words) + struct.pack("<Q", state)
+
+
+@gpu
+def test_fse_decode_last_bytes_path_vs_oracle(oracle):
+    """k_fse_dec through renormalize_decode's single-byte branch (fse.rs:726-729):
+    word areas of 1, 2, 3, 5, 6 and 7 bytes, so that the last renormalisations
+    of the stream read single bytes with 3, 2 and 1 bytes left (the fse.rs:1621-1635
+    case is the 2-byte area). Status and bytes equal the oracle's."""
+    import random
+    rng = random.Random(1635)
+    cases = 0
+    for area in (1, 2, 3, 5, 6, 7):
+        for nsym in (256, 16, 2):
+            for _ in range(4):
+                words = bytes(rng.randrange(256) for _ in range(area))
+                # small states renormalise at once; 2^16.. states after a few symbols
+                state = rng.choice([100, 1, 0, 4095, 65535, rng.randrange(1 << 16, 1 << 24),
+                                    rng.randrange(1 << 24, 1 << 48)])
+                n = rng.choice([1, 2, 3, 8, 40])
+                s = _f5_with_word_area(words, state, n, nsym)
+                try:
+                    want = oracle.fse_decompress(s)
+                except oracle.OracleError:
+                    want = None
+                try:
+                    got = zr.fse_decompress(s)
+                except zr.ZiporaError:
+                    got = None
+                assert got == want, f"area {area} nsym {nsym} state {state} n {n}"
+                cases += want is not None
+    assert cases > 0

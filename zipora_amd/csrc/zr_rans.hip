@@ -173,6 +173,7 @@ __device__ __forceinline__ void hist_tab_tail(uint32_t *hist, RansDTab *tab, uin
     if (threadIdx.x == 0) last = tab_arrive(epoch, blockIdx.x, gridDim.x) ? 1u : 0u;
     __syncthreads();
     if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's adds before the exchange
     const uint32_t f = __hip_atomic_exchange(&hist[threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tab_build(f, tab, h);
 }
@@ -430,9 +431,12 @@ __device__ unsigned int g_tab_tick[TT_SLOTS][9];
 __device__ __noinline__ bool tab_arrive(uint64_t epoch, uint32_t g, uint32_t nwg) {
     unsigned int *const t = g_tab_tick[epoch % TT_SLOTS];
     const uint32_t sh = g & 7, in_sh = (nwg - sh + 7) / 8, nsh = min(nwg, 8u);
-    if (__hip_atomic_fetch_add(&t[sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 != in_sh) return false;
+    // release: this workgroup's histogram adds (performed: vmcnt(0) before the
+    // call) are ordered before its ticket; acq_rel at the top counter chains
+    // the shards' releases to the last workgroup, which acquires (hist_tab_tail)
+    if (__hip_atomic_fetch_add(&t[sh], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) + 1 != in_sh) return false;
     __hip_atomic_store(&t[sh], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_fetch_add(&t[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 != nsh) return false;
+    if (__hip_atomic_fetch_add(&t[8], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 != nsh) return false;
     __hip_atomic_store(&t[8], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
 }

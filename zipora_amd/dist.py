@@ -130,8 +130,12 @@ def shared_table_comm(nranks, rank):
     the torch.distributed group's on every rank (reported on stderr; the run
     goes on). The ranks agree twice: before the collective init (a rank that
     has no id or no zr_comm keeps every rank out of it) and after it (a rank
-    whose init failed makes every rank destroy its communicator and fall back
-    together, so no two ranks run the exchange on different collectives)."""
+    whose init failed on the Python side, e.g. the library call returned an
+    error, makes every rank destroy its communicator and fall back together,
+    so no two ranks run the exchange on different collectives). A failure
+    INSIDE ncclCommInitRank is not covered: that init is collective, so the
+    other ranks may stay blocked in their own init and never reach the second
+    agreement (RCCL's own init timeout then ends them)."""
     import sys
     uid, err = None, None
     if rank == 0:
@@ -152,7 +156,10 @@ def shared_table_comm(nranks, rank):
         if _all_ranks(1 if comm is not None else 0):
             return comm
         if comm is not None:
-            comm.close()
+            try:
+                comm.close()
+            except Exception as e:  # noqa: BLE001  (the fallback below still applies)
+                err = err or f"zr_comm_destroy failed: {e}"
             err = err or "another rank's zr_comm_init failed"
     print(f"zipora_amd: no zr_comm communicator ({err}); histogram all-reduce on torch.distributed",
           file=sys.stderr)
