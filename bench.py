@@ -51,6 +51,9 @@ def parse():
                         "main stream) while the histogram + table of the next one run on a second stream")
     p.add_argument("--enc-width", type=int, default=256, choices=[256, 1024],
                    help="rans: the xN encoder's workgroup width (zr_rans_set_encoder_width)")
+    p.add_argument("--dec-ring", type=int, default=0, choices=[0, 1, 2],
+                   help="rans: the xN decoder's ring (zr_rans_set_decoder_ring): 0 auto, 1 VGPR-staged "
+                        "(k_dec_xn_fast), 2 LDS-DMA chunks (k_dec_xn_dma, 8 waves per SIMD)")
     p.add_argument("--enc-split", type=int, default=None, choices=[0, 1, 2, 3],
                    help="rans: encode a wide batch in two parts (the first q/4 of the buffers, then the rest), "
                         "the second part's encoder and the first part's compaction in one dispatch "
@@ -841,6 +844,9 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     single = B == 1
     literal = single and N == 4096
     wl = "rans_literal" if literal else f"rans_n2e{N.bit_length() - 1}" if single else "rans"
+    syms = dict(RANS_SYMS)  # the decode kernel this batch ran (zr_rans_decoder_kernel)
+    if hasattr(L, "zr_rans_decoder_kernel"):
+        syms["rans_decode"] = L.zr_rans_decoder_kernel(B, N).decode()
     rans_bytes = {"rans_encode": total + comp_bytes, "rans_decode": comp_bytes + total,
                   "rans_compact": 2 * comp_bytes, "histogram": total}
     if split:
@@ -884,9 +890,9 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
                       if pipe else {})},
         # the dominant kernel's roofline (the encoder on the headline): algorithmic bytes
         # per launch = N_in read + C written (encode, decode), 2 C (compaction), N_in (histogram)
-        "roofline": _roofline(dom, dom_ms, rans_bytes, wl, RANS_SYMS, kms),
+        "roofline": _roofline(dom, dom_ms, rans_bytes, wl, syms, kms),
         # the decoder's, from the instrumented pass (the decode half of the step)
-        "roofline_decode": _roofline("rans_decode", tms["rans_decode"], rans_bytes, wl, RANS_SYMS, kms),
+        "roofline_decode": _roofline("rans_decode", tms["rans_decode"], rans_bytes, wl, syms, kms),
         # the whole step against the spec peak: (3 N_in + 2 C) / step time
         "step_frac": round((3 * total + 2 * comp_bytes) / (dt / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
         "kernels_ms": kms, "kernels_ms_source": KMS_SOURCE,
@@ -1066,6 +1072,8 @@ def main():
     L.zr_set_device(local)
     if hasattr(L, "zr_rans_set_encoder_width") and L.zr_rans_set_encoder_width(args.enc_width):
         raise SystemExit(f"encoder width {args.enc_width} refused")
+    if args.dec_ring and L.zr_rans_set_decoder_ring(args.dec_ring):
+        raise SystemExit(f"decoder ring {args.dec_ring} refused")
     if args.enc_split is not None and L.zr_rans_set_encode_split(args.enc_split):
         raise SystemExit(f"encode split {args.enc_split} refused")
 

@@ -169,6 +169,17 @@ int32_t zr_rans_dtab_from_hist_consume_dev(uint32_t *hist_dev, uint32_t n_tables
  * slot, and a table would then be built before its histogram is complete). */
 int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *batch, uint32_t *hist_dev,
                                    void *dtab_dev, void *stream);
+/* Tuning (no reference counterpart): the xN decoder's ring for batches of more
+ * than 2^16 streams, process-wide. 0 (default) and 1: the VGPR-staged ring
+ * decoder (one 1024-lane workgroup per CU, 4 waves per SIMD); 2: the LDS-DMA
+ * ring decoder (two 1024-lane workgroups per CU, 8 waves per SIMD, N >= 64),
+ * measured slower. Both decode the same format
+ * bit for bit (rans.rs:555-651). */
+int32_t zr_rans_set_decoder_ring(int32_t ring);
+/* The name of the xN decode kernel a batch of n_buffers x n_streams (every
+ * buffer at least n_streams bytes) runs under the current setting (reports and
+ * profiles; a static string). */
+const char *zr_rans_decoder_kernel(uint32_t n_buffers, uint32_t n_streams);
 /* Tuning (no reference counterpart): the workgroup width of the xN encoder for
  * batches of more than 2^16 streams, process-wide: 256 (default) or 1024 (one
  * workgroup per CU with 16 conflict-free copies of the encode table; used

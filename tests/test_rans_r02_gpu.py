@@ -706,11 +706,12 @@ def test_decode_errors_two_level_arrival(zr, oracle, N, B, n, first_bad):
         k = b % 3
         if k == 0:  # truncated: the last streams run out of bytes
             enc_len[b] = L - rnd.randrange(1, 8)
-        elif k == 1:  # 5 bytes moved between two streams of the last set
+        elif k == 1:  # bytes moved between two streams of the last set
             s = rnd.randrange(first_bad, N - 1)
             ls, ls1 = o + 8 * N + 4 * s, o + 8 * N + 4 * (s + 1)
-            host[ls:ls + 4] = (u32(host, ls) - 5).to_bytes(4, "little")
-            host[ls1:ls1 + 4] = (u32(host, ls1) + 5).to_bytes(4, "little")
+            mv = min(5, u32(host, ls))  # (short streams: N = 12288 codes 6 symbols each)
+            host[ls:ls + 4] = (u32(host, ls) - mv).to_bytes(4, "little")
+            host[ls1:ls1 + 4] = (u32(host, ls1) + mv).to_bytes(4, "little")
         else:  # a state of the last set below 2^16
             s = rnd.randrange(first_bad, N)
             host[o + 8 * s:o + 8 * s + 8] = rnd.randrange(1, 1 << 16).to_bytes(8, "little")

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(FW, W) void kdec(const uint8_t *__restrict__ enc, u
     const uint32_t end = 64 + (s + 1) * S;  // stream s: enc[64 + s*S, 64 + (s+1)*S)
     uint32_t x = ((s * 2654435761u) & 0xFFFFFFu) | 0x10000u;
     char *const ringb = reinterpret_cast<char *>(lds + TABW);
-    constexpr bool DMA = MODE == 2 || MODE == 5, REL = MODE == 2;
+    constexpr bool DMA = MODE == 2 || MODE == 5 || MODE == 6 || MODE == 7, REL = MODE != 5;
     // DMA modes: the wave's ring, 4 rows of 1 KiB; lane slot lane * 16
     char *const wring = ringb + wv * 4096;
     const uint32_t lb = (uint32_t)(uintptr_t)(wring) + lane * 16;  // (LDS byte address)
@@ -59,11 +59,14 @@ __global__ __launch_bounds__(FW, W) void kdec(const uint8_t *__restrict__ enc, u
     auto dma_row = [&](uint32_t y0, bool m) __attribute__((always_inline)) {
         // y0: chunk base coordinate (16-aligned); row (y0 >> 4) & 3
         const uint32_t r = (y0 >> 4) & 3;
+        // MODE 6: the same instruction stream, sources in a 512 KiB L2-resident region
+        // (lane-distinct lines): timing only
+        const uintptr_t gsrc = MODE == 6 ? (uintptr_t)enc + ((tid * 128 + (y0 & 0x70)) & 0x7FFFF) : gb + y0;
         for (uint32_t rr = 0; rr < 4; rr++) {
             const bool mm = m && r == rr;
             if (__builtin_amdgcn_ballot_w64(mm)) {
                 if (mm)
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gb + y0),
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(gsrc),
                                                      reinterpret_cast<void *>(wring + rr * 1024), 16, 0, 0);
             }
         }
@@ -140,7 +143,13 @@ __global__ __launch_bounds__(FW, W) void kdec(const uint8_t *__restrict__ enc, u
         if (MODE != 0) {
             const uint32_t y = p8 >> 3;
             const bool issue = (int32_t)(y - ylo) < 48;
-            if constexpr (DMA) {
+            if constexpr (MODE == 7) {
+                // timing only: 64 B (4 chunks of one half line) every 4th boundary
+                if ((t & 3) == 0) {
+                    ylo -= 64;
+                    for (uint32_t k = 0; k < 4; k++) dma_row(ylo + 16 * k, true);
+                }
+            } else if constexpr (DMA) {
                 if (issue) ylo -= 16;
                 dma_row(ylo, issue);
             } else {
@@ -208,7 +217,7 @@ void run(const char *name, const uint8_t *enc, uint8_t *raw, const uint32_t *tab
     if (e != hipSuccess) { printf("%s: %s\n", name, hipGetErrorString(e)); exit(1); }
     // check a few streams
     int bad = 0;
-    if (MODE != 0) {
+    if (MODE != 0 && MODE != 6 && MODE != 7) {
         std::vector<uint8_t> o(1u << 28);
         hipMemcpy(o.data(), raw, 1u << 28, hipMemcpyDeviceToHost);
         std::vector<uint8_t> r;
@@ -253,6 +262,8 @@ int main(int argc, char **argv) {
     }
     if (which < 0 || which == 3) { run<3, 4>("VGPR staging, dword rows", enc, raw, tab, henc, htab); run<3, 8>("VGPR staging, dword rows", enc, raw, tab, henc, htab); }
     if (which < 0 || which == 2) { run<2, 4>("DMA x4, stream-relative chunks", enc, raw, tab, henc, htab); run<2, 8>("DMA x4, stream-relative chunks", enc, raw, tab, henc, htab); }
+    if (which < 0 || which == 6) { run<6, 4>("DMA x4, L2-resident sources", enc, raw, tab, henc, htab); run<6, 8>("DMA x4, L2-resident sources", enc, raw, tab, henc, htab); }
+    if (which < 0 || which == 7) { run<7, 4>("DMA x4, 64 B per 64 steps", enc, raw, tab, henc, htab); run<7, 8>("DMA x4, 64 B per 64 steps", enc, raw, tab, henc, htab); }
     if (which < 0 || which == 5) { run<5, 4>("DMA x4, aligned chunks", enc, raw, tab, henc, htab); run<5, 8>("DMA x4, aligned chunks", enc, raw, tab, henc, htab); }
     return 0;
 }

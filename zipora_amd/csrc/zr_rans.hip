@@ -499,6 +499,20 @@ static std::atomic<uint32_t> g_enc_width{256};
 #define ZR_ENC_SPLIT_DEFAULT 0
 #endif
 static bool enc_w1024() { return g_enc_width.load(std::memory_order_relaxed) == 1024; }
+// the xN decoder's ring for batches of more than 2^16 streams: 0 auto and 1:
+// the VGPR-staged ring (k_dec_xn_fast), 2: the LDS-DMA ring (k_dec_xn_dma, 8
+// waves per SIMD; zr_rans_set_decoder_ring). Round 5 measured the DMA ring
+// 1.5-1.9x slower at N = 2^18..2^20 on one 256 MiB buffer (its 64-B rings
+// refill 16 B at a time: 3.6-5.5x read over-fetch; profiles/r05_dec_curve.txt,
+// DESIGN.md section 4), so auto never picks it; it stays as a tested opt-in
+static std::atomic<int> g_dec_ring{0};
+// (batches of more than 2^16 streams; N >= 64: the header below a buffer's
+// first stream is >= 768 bytes, more than a lane's chunk requests reach below
+// its stream)
+static bool dec_uses_dma(uint32_t B, uint32_t N) {
+    (void)B;
+    return N >= 64 && g_dec_ring.load(std::memory_order_relaxed) == 2;
+}
 // split encode (zr_rans_set_encode_split): the xN encode of a wide batch as
 // encoder(lower half) -> encoder(upper half) + compaction(lower half) in one
 // dispatch (k_enc_cmp_fused) -> compaction(upper half)
@@ -1567,6 +1581,9 @@ __global__ __launch_bounds__(256) void k_dec_hdr(const uint8_t *enc, KArgs a, Ra
 //     store per wave, row offset in an SGPR, no VALU address work.
 // ----------------------------------------------------------------------
 constexpr int RR = 32;   // ring rows (dwords) per lane
+#ifndef ZR_DEC_PK
+#define ZR_DEC_PK 1  // full waves over 4-aligned output store 4 steps' bytes as one dword per lane
+#endif
 #ifndef ZR_DEC_T8
 #define ZR_DEC_T8 1  // the 1024-lane decoder reads 8-byte slot entries (f | sym << 24, slot - start)
 #endif
@@ -1663,9 +1680,17 @@ __device__ __noinline__ void dec_arrive(uint64_t *wbase, uint64_t epoch, bool er
     if (arrive_word(wbase, tag, err, nwg)) *status = err ? ZR_INVALID_INPUT : ZR_OK;
 }
 
-template <int FW, int ABL, bool WT = false>
-__global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
-                                               uint32_t nblkF, uint64_t epoch) {
+// RD: the ring design. 0: the VGPR-staged dword-row ring above (k_dec_xn_fast);
+// 1: k_dec_xn_dma's LDS-DMA chunk ring (4-byte slot entries, 80 KiB per
+// workgroup: two 1024-lane workgroups per CU, 8 waves per SIMD)
+template <int FW, bool WT, int RD>
+constexpr uint32_t dec_lds_words() {
+    return RD == 1 ? TOTFREQ + 16 * FW : (WT ? 2 : 1) * TOTFREQ + (RR + (!(WT && FW == 1024) ? 1 : 0)) * FW;
+}
+template <int FW, int ABL, bool WT, int RD>
+__device__ __forceinline__ void dec_xn_body(const uint8_t *enc, uint8_t *raw, const KArgs &a, const RansWork &w,
+                                            uint32_t nblkF, uint64_t epoch, uint32_t *lds) {
+    static_assert(RD == 0 || (FW == 1024 && !WT), "the DMA ring: 1024-lane workgroups, 4-byte entries");
     const uint32_t b = blockIdx.x / nblkF, blkF = blockIdx.x % nblkF;
     const uint64_t dbg_t0 = (ABL & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t dbg_c0 = (ABL & 8) ? __builtin_amdgcn_s_memtime() : 0;
@@ -1688,7 +1713,6 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
     // slot entry with the symbol in its top byte (wide shape, 8-byte entries)
     constexpr bool MIR = !(WT && FW == 1024);
     constexpr bool SH = WT && FW == 1024;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[TABW + (RR + (MIR ? 1 : 0)) * FW];
     uint32_t *ring = lds + TABW;
     // scan scratch and flag alias the ring (used before it is filled)
     unsigned long long *sh = reinterpret_cast<unsigned long long *>(ring);
@@ -1863,375 +1887,563 @@ __global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t 
         finish();
         return;
     }
-    const uintptr_t pend = sb + L;
-    const uintptr_t lo_lim = ((uintptr_t)e) & ~(uintptr_t)63;
-    auto clampa = [&](uintptr_t p) -> uintptr_t { return p > lo_lim ? p : lo_lim; };
-    uint32_t *lring = ring + tid;
-    // write the 64-B segment at absolute address g (64-aligned; cK = bytes g+16K..)
-    auto put_seg = [&](uint32_t g, const v4u c0, const v4u c1, const v4u c2, const v4u c3) __attribute__((always_inline)) {
-        const uint32_t r0 = ((g >> 2) + 1) & (RR - 1);  // 1 or 17
-        uint32_t *p = lring + r0 * FW;
-        p[0 * FW] = c0.x; p[1 * FW] = c0.y; p[2 * FW] = c0.z; p[3 * FW] = c0.w;
-        p[4 * FW] = c1.x; p[5 * FW] = c1.y; p[6 * FW] = c1.z; p[7 * FW] = c1.w;
-        p[8 * FW] = c2.x; p[9 * FW] = c2.y; p[10 * FW] = c2.z; p[11 * FW] = c2.w;
-        p[12 * FW] = c3.x; p[13 * FW] = c3.y; p[14 * FW] = c3.z;
-        if (MIR) p[15 * FW] = c3.w;             // row 16, or the mirror row 32
-        lring[((r0 + 15) & (RR - 1)) * FW] = c3.w;  // row 0 itself (r0 = 17; r0 = 1: row 16 again)
-    };
-    // prologue: the 64-B segment holding the last stream byte and the one below
-    const uintptr_t g1 = (pend - 1) & ~(uintptr_t)63;
-    {
-        // (addresses rebased on e: global loads, not flat)
-        const v4u *p1 = reinterpret_cast<const v4u *>(e + (int64_t)(clampa(g1) - (uintptr_t)e));
-        const v4u *p0 = reinterpret_cast<const v4u *>(e + (int64_t)(clampa(g1 - 64) - (uintptr_t)e));
-        const v4u a0 = p1[0], a1 = p1[1], a2 = p1[2], a3 = p1[3];
-        const v4u b0 = p0[0], b1 = p0[1], b2 = p0[2], b3 = p0[3];
-        put_seg((uint32_t)g1, a0, a1, a2, a3);
-        put_seg((uint32_t)(g1 - 64), b0, b1, b2, b3);
-    }
-    // positions are tracked as byte address * 8 (mod 2^32): the ring only needs the
-    // low bits and comparisons use 32-bit differences.
-    // PF (the 64-lane shape, one wave per SIMD, issue-bound): the lowest resident
-    // byte is kept as byte * 8 and as a signed offset from lo_lim (stream sets are
-    // < 2^31 bytes), so the refill address is one 32-bit max and one add, and the
-    // in-flight state is one flag per staging set. The 1024-lane shape keeps the
-    // 64-bit address and one (flag, tile) pair: measured 2.5 % faster there, the
-    // PF form 3.5 % faster at 64 lanes
-    constexpr bool PF = FW == 64;
-    uintptr_t lo64 = g1 - 64;                     // !PF: lowest resident byte
-    uint32_t lo8 = (uint32_t)(g1 - 64) << 3;      // PF: lowest resident byte * 8
-    int32_t lo = (int32_t)((g1 - 64) - lo_lim);  // PF: the same, from lo_lim (>= -64)
-    uint32_t pos8 = (uint32_t)pend << 3;  // bytes [.., pos) not yet consumed
-    uint32_t x = (uint32_t)X;
-    // D: the 4 stream bytes below p (byte p-1 on top)
-    auto readD = [&](uint32_t p8) -> uint32_t __attribute__((always_inline)) {
-        const uint32_t r = (p8 >> 5) & (RR - 1);
-        if constexpr (!MIR) {  // rows r and r + 1 (mod 32): byte offsets in the ring, the lane's column added
-            const uint32_t o0 = (p8 << 7) & ((RR - 1) * FW * 4), o1 = (o0 + FW * 4) & ((RR - 1) * FW * 4);
-            const char *base = reinterpret_cast<const char *>(ring) + tid * 4;
-            return __builtin_amdgcn_alignbit(*reinterpret_cast<const uint32_t *>(base + o1),
-                                             *reinterpret_cast<const uint32_t *>(base + o0), p8);
-        }
-        const uint32_t *q = lring + r * FW;
-        return __builtin_amdgcn_alignbit(q[FW], q[0], p8);
-    };
-    // one decode step (rans.rs:472-507): renormalise from window D, decode, return
-    // the slot entry; hi/lo are the shifted (x : D) pair, sft = 8 + 8 * bytes consumed
-    auto step = [&](uint32_t D, uint32_t &hi, uint32_t &lo, uint32_t &sft) -> uint32_t __attribute__((always_inline)) {
-        sft = __builtin_clz(x) & 24;
-        const uint64_t t = ((((uint64_t)x) << 32) | D) << sft;
-        hi = (uint32_t)(t >> 32);
-        lo = (uint32_t)t;
-        if (WT && !(ABL & 2)) {  // 8-byte entry: x = f * (x >> 12) + (slot - start), sym in the top byte
-            const v2u e2 = *reinterpret_cast<const v2u *>(reinterpret_cast<const char *>(lds) + ((hi >> 5) & 0x7FF8));
-            x = __umul24(e2.x, hi >> 20) + e2.y;
-            return SH ? e2.x : e2.x >> 24;
-        }
-        const uint32_t ent = (ABL & 2) ? (hi & 0x0FFFFF00u) | 0x01000000u
-                                       : *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) +
-                                                                             ((hi >> 6) & 0x3FFC));
-        x = __umul24(ent >> 20, hi >> 20) + ((ent >> 8) & 0xFFF);
-        // sensitivity probes (diagnostic builds): 16 = two more VALU on the step's
-        // chain, 32 = two more VALU off it
-        if (ABL & 16) asm volatile("v_add_u32 %0, 0, %0\n\tv_add_u32 %0, 0, %0" : "+v"(x));
-        if (ABL & 32) {
-            uint32_t d0, d1;
-            asm volatile("v_mov_b32 %0, 0\n\tv_mov_b32 %1, 1" : "=v"(d0), "=v"(d1));
-        }
-        return ent;
-    };
-    uint32_t sink = 0;
-    // staging registers of the segment loads issued at even / odd boundaries
-    v4u e0 = {0, 0, 0, 0}, e1 = e0, e2 = e0, e3 = e0, o0 = e0, o1 = e0, o2 = e0, o3 = e0;
-    bool pnd_e = false, pnd_o = false;  // PF: a segment in flight in the even / odd staging set
-    bool pnd = false;                   // !PF: a segment in flight, fetched at boundary ptile
-    uint32_t ptile = 0;
-    bool bad = false;
-    const uint64_t wbase = (uint64_t)blkF * FW + (tid & ~63u);
-    const bool wave_live = wbase < N;       // wave-uniform
-    const bool wave_all = wbase + 64 <= N;  // wave-uniform
-    uint8_t *outb = raw + a.raw_off[b] + (size_t)blkF * FW;
-    // output rows are addressed through a descriptor rebased every tile, so the
-    // 32-bit buffer offsets cover any buffer size. A lane without a stream
-    // stores at offset 2^31 (+ the row), beyond the descriptor's 2^31 - 1
-    // records: the hardware drops it, so the stores need no exec mask.
-    __amdgpu_buffer_rsrc_t orsrc = byte_rsrc(outb);
-    const uint32_t voff = active ? tid : 0x80000000u;
-    // packed stores (wide shape): lane 4q + r of a wave writes row r of streams
-    // 4q..4q+3; the transpose's byte selectors by the lane's place in its quad
-    const uint32_t voff_pk = (tid & ~3u) + (tid & 3u) * N;
-    const uint32_t psel1 = (tid & 2) ? 0x03020706u : 0x05040100u;  // 16-bit halves with lane ^ 2
-    const uint32_t psel2 = (tid & 1) ? 0x03070105u : 0x06020400u;  // bytes with lane ^ 1
-    // PF: DT2-step tiles with k0 + DT2 < cmax. Wide shape: TW-step tiles over
-    // the rows every stream of the buffer has (n / N of them), the rest in the
-    // tail loop
-    constexpr uint32_t TW = 32;
-    const uint32_t nfull = PF ? (uint32_t)((cmax - 1) / DT2) : (uint32_t)((n / N) / TW);
-    auto lov8 = [&]() -> uint32_t { return PF ? lo8 : (uint32_t)lo64 << 3; };
-    // a segment lands: the staging set becomes the 64 bytes below the resident ones
-    auto land = [&](const v4u c0, const v4u c1, const v4u c2, const v4u c3) __attribute__((always_inline)) {
-        if constexpr (PF) {
-            lo8 -= 512;
-            lo -= 64;
-            put_seg(lo8 >> 3, c0, c1, c2, c3);
-        } else {
-            lo64 -= 64;
-            if (!(ABL & 64)) put_seg((uint32_t)lo64, c0, c1, c2, c3);
-        }
-    };
-
-    // lanes that fetch nothing at a boundary load a line of the table instead
-    // (L2-resident, one request per wave; a lane-private re-load measured 2x
-    // slower at 1024 lanes per CU): the loads are issued unconditionally so
-    // that no control flow ever merges a staging register still in flight
-    const uintptr_t dummy = (uintptr_t)T->slot + 64 * (tid >> 6);
-
-    // tile boundary t, staging set (s0..s3) = the set of parity t & 1, pmine its
-    // in-flight flag
-    auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3, bool &pmine, bool pother) __attribute__((always_inline)) {
-        // every read of the previous tile was at or above pos - 4 (the no-refill
-        // ablation reads stale ring bytes on purpose: no fallback there)
-        bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
-        if (t >= 2) {
-            // wait for the loads of boundary t-2: younger are the 16 stores of tile
-            // t-2, the 4 loads of boundary t-1 and the 16 stores of tile t-1 (every
-            // wave issues all of them: lanes without a stream store out of range)
-            if (ABL & 1)
-                asm volatile("s_waitcnt vmcnt(4)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
-            else
-                asm volatile("s_waitcnt vmcnt(36)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
-            if (PF ? pmine : pnd && ptile + 2 == t) {  // the segment this set fetched at boundary t - 2
-                land(s0, s1, s2, s3);
-                pmine = pnd = false;
-            }
-        }
-        // a lane with <= 64 unread resident bytes fetches the segment below
-        const bool issue =
-            !(ABL & 4) && active && (PF ? !pmine && !pother : !pnd) && (int32_t)(pos8 - lov8()) <= 64 * 8;
-        const uintptr_t g = !issue ? dummy : PF ? lo_lim + (uint32_t)max(lo - 64, 0) : clampa(lo64 - 64);
-        asm_load16(s0, g);
-        asm_load16_off<16>(s1, g);
-        asm_load16_off<32>(s2, g);
-        asm_load16_off<48>(s3, g);
-        if constexpr (PF) {
-            pmine = pmine || issue;
-        } else if (issue) {
-            pnd = true;
-            ptile = t;
-        }
-    };
-    // DT2 steps in pairs; one ring read per pair
-    auto tile = [&](uint32_t t) __attribute__((always_inline)) {
-        uint32_t D = readD(pos8);
-        orsrc = byte_rsrc(outb + (uint64_t)t * DT2 * N);
-        uint32_t row = 0;
+    if constexpr (RD == 1) {
+        // ---- LDS-DMA chunk ring (k_dec_xn_dma). The stream is read through
+        // coordinates y = A - pend + YB (A: byte address; the stream's end at
+        // y = YB, a multiple of 64), so chunk boundaries sit at the same place
+        // relative to every stream's end and lanes that consume at the same
+        // rate refill the same ring row at the same boundary. Per wave a ring of
+        // 4 rows x 1 KiB; lane l's 16 bytes of coordinates [16k, 16k + 16) sit
+        // in row k & 3 at byte 16 l: exactly what one global_load_lds_dwordx4
+        // of the wave writes (wave-uniform LDS base + lane * 16), with no VGPR
+        // staging and no landing writes. A window read takes the two dwords of
+        // coordinates [y - 4, y + 4) (two rows when they straddle a chunk).
+        constexpr uint32_t YB = 1u << 20;
+        const uint32_t lane = tid & 63, wv = tid >> 6;
+        char *const wring = reinterpret_cast<char *>(ring) + wv * 4096;
+        const uint32_t lb = (uint32_t)(uintptr_t)wring + lane * 16;  // (LDS byte address)
+        const uintptr_t pend = sb + L;
+        const uintptr_t gsrc = pend - YB;  // address of coordinate 0
+        // chunk at coordinate y0 (16-aligned) into row (y0 >> 4) & 3 for lanes m;
+        // one DMA instruction per row some lane needs (lanes at the same rate: one)
+        auto dma = [&](uint32_t y0, bool m) __attribute__((always_inline)) {
+            const uint32_t r = (y0 >> 4) & 3;
+            const uintptr_t g = gsrc + y0;
 #pragma unroll
-        for (int j = 0; j < DT2 / 2; j++) {
-            uint32_t hA, lA, sA, hB, lB, sB;
-            const uint32_t eA = step(D, hA, lA, sA);
-            const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
-            uint32_t used;  // sA + sB - 16 = 8 * bytes consumed by the pair
-            asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
-            pos8 -= used;
-            if (j + 1 < DT2 / 2) D = readD(pos8);
-            if (ABL & 1) {
-                sink += eA ^ eB;
-            } else {  // no exec mask: a lane without a stream stores out of range (dropped)
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, voff, row, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eB, orsrc, voff, row + N, 0);
+            for (uint32_t rr = 0; rr < 4; rr++) {
+                const bool mm = m && r == rr;
+                if (__builtin_amdgcn_ballot_w64(mm)) {
+                    if (mm)
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g),
+                                                         reinterpret_cast<void *>(wring + rr * 1024), 16, 0, 0);
+                }
             }
-            row += 2 * N;
-        }
-    };
-
-    // ---- wide shape (1024 lanes per CU, 4 waves per SIMD): TW = 32-step tiles;
-    // a refill issued at boundary t lands at boundary t + 1 (32 steps, a few us,
-    // cover the load: one staging set, half the boundaries of 16-step tiles).
-    // Full waves over 4-aligned output pack the bytes of 4 steps into one dword
-    // store per lane: the quad's 4 x 4 bytes (lane r of the quad holds rows
-    // 4g..4g+3 of its stream) are transposed by two DPP lane swaps + v_perm,
-    // so lane 4q + r stores row 4g + r of streams 4q..4q+3: 8 dword stores per
-    // tile instead of 32 byte stores.
-    auto tile_w = [&](uint32_t t, bool pk) __attribute__((always_inline)) {
-        uint32_t D = readD(pos8);
-        orsrc = byte_rsrc(outb + ((ABL & 256) ? 0 : (uint64_t)t * TW * N));
-        uint32_t row = 0, pk0 = 0;
+        };
+        // ylo: the lowest chunk requested; yland8: the lowest landed, * 8
+        uint32_t ylo = YB - 64;
 #pragma unroll
-        for (int j = 0; j < (int)TW / 2; j++) {
-            uint32_t hA, lA, sA, hB, lB, sB;
-            const uint32_t eA = step(D, hA, lA, sA);
-            const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
-            uint32_t used;
-            asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
-            pos8 -= used;
-            if (j + 1 < (int)TW / 2) D = readD(pos8);
-            if (ABL & 1) {
-                sink += eA ^ eB;
-            } else if (pk) {
-                // (SH: the symbols are the entries' top bytes)
-                if ((j & 1) == 0) {
-                    pk0 = __builtin_amdgcn_perm(eB, eA, SH ? 0x0c0c0703u : 0x0c0c0400u);  // [eA, eB, 0, 0]
+        for (uint32_t k = 0; k < 4; k++) dma(ylo + 16 * k, active);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t yland8 = ylo << 3;
+        uint32_t p8 = YB << 3;  // position * 8: bytes [.., y) not yet consumed
+        uint32_t x = (uint32_t)X;
+        auto lds_u32 = [&](uint32_t addr) -> uint32_t {
+            return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(addr);
+        };
+        // D: the 4 stream bytes below y (byte y-1 on top)
+        auto readD = [&](uint32_t q8) -> uint32_t {
+            const uint32_t y1 = q8 >> 3, y0 = y1 - 4;
+            const uint32_t a1 = (((y1 >> 4) & 3) << 10) | (y1 & 12) | lb;
+            const uint32_t a0 = (((y0 >> 4) & 3) << 10) | (y0 & 12) | lb;
+            return __builtin_amdgcn_alignbit(lds_u32(a1), lds_u32(a0), q8);
+        };
+        // one decode step (rans.rs:472-507), as k_dec_xn_fast's 4-byte-entry step
+        auto step = [&](uint32_t D, uint32_t &hi, uint32_t &lo, uint32_t &sft) -> uint32_t {
+            sft = __builtin_clz(x) & 24;
+            const uint64_t t = ((((uint64_t)x) << 32) | D) << sft;
+            hi = (uint32_t)(t >> 32);
+            lo = (uint32_t)t;
+            const uint32_t ent =
+                *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + ((hi >> 6) & 0x3FFC));
+            x = __umul24(ent >> 20, hi >> 20) + ((ent >> 8) & 0xFFF);
+            return ent;
+        };
+        bool bad = false;
+        const uint64_t wbase = (uint64_t)blkF * FW + (tid & ~63u);
+        const bool wave_live = wbase < N;
+        const bool wave_all = wbase + 64 <= N;
+        uint8_t *outb = raw + a.raw_off[b] + (size_t)blkF * FW;
+        __amdgpu_buffer_rsrc_t orsrc = byte_rsrc(outb);
+        const uint32_t voff = active ? tid : 0x80000000u;
+        const uint32_t voff_pk = (tid & ~3u) + (tid & 3u) * N;
+        const uint32_t psel1 = (tid & 2) ? 0x03020706u : 0x05040100u;
+        const uint32_t psel2 = (tid & 1) ? 0x03070105u : 0x06020400u;
+        constexpr uint32_t TD = 16;  // steps per tile
+        const uint32_t nfull = (uint32_t)((n / N) / TD);
+        // a boundary: the chunks of the previous boundary have landed (the wave's
+        // counted vmcnt orders its own ds_reads behind its DMA); check that the
+        // previous tile consumed only landed bytes; request every chunk whose
+        // row is free (all its old bytes consumed: y <= chunk + 64), at most two
+        auto refill = [&]() __attribute__((always_inline)) {
+            bad |= !(ABL & 4) && active && (int32_t)(p8 - yland8) < 0;
+            yland8 = ylo << 3;
+#pragma unroll
+            for (int rnd = 0; rnd < 2; rnd++) {
+                const bool m = !(ABL & 4) && active && (int32_t)(p8 - ((ylo + 48) << 3)) <= 0;
+                if (!__builtin_amdgcn_ballot_w64(m)) break;
+                const uint32_t yn = m ? ylo - 16 : ylo;
+                dma(yn, m);
+                ylo = yn;
+            }
+        };
+        auto tile = [&](uint32_t t, bool pk) __attribute__((always_inline)) {
+            uint32_t D = readD(p8);
+            orsrc = byte_rsrc(outb + (uint64_t)t * TD * N);
+            uint32_t row = 0, pk0 = 0;
+#pragma unroll
+            for (int j = 0; j < (int)TD / 2; j++) {
+                uint32_t hA, lA, sA, hB, lB, sB;
+                const uint32_t eA = step(D, hA, lA, sA);
+                const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
+                uint32_t used;
+                asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
+                p8 -= used;
+                if (j + 1 < (int)TD / 2) D = readD(p8);
+                if (ABL & 1) {
+                    bad |= (eA ^ eB) == 0x9E3779B9u;
+                } else if (pk) {
+                    if ((j & 1) == 0) {
+                        pk0 = __builtin_amdgcn_perm(eB, eA, 0x0c0c0400u);  // [eA, eB, 0, 0]
+                    } else {
+                        uint32_t q = __builtin_amdgcn_perm(eB, eA, 0x04000c0cu) | pk0;
+                        uint32_t xx = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0x4E, 0xF, 0xF, false);
+                        q = __builtin_amdgcn_perm(xx, q, psel1);
+                        xx = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0xB1, 0xF, 0xF, false);
+                        q = __builtin_amdgcn_perm(xx, q, psel2);
+                        __builtin_amdgcn_raw_buffer_store_b32(q, orsrc, voff_pk, row - 2 * N, 0);
+                    }
                 } else {
-                    uint32_t q = __builtin_amdgcn_perm(eB, eA, SH ? 0x07030c0cu : 0x04000c0cu) | pk0;  // rows 4g..4g+3
-                    uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0x4E, 0xF, 0xF, false);  // lane ^ 2
-                    q = __builtin_amdgcn_perm(x, q, psel1);
-                    x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0xB1, 0xF, 0xF, false);  // lane ^ 1
-                    q = __builtin_amdgcn_perm(x, q, psel2);
-                    __builtin_amdgcn_raw_buffer_store_b32(q, orsrc, voff_pk, (ABL & 256) ? 0 : row - 2 * N, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, voff, row, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eB, orsrc, voff, row + N, 0);
+                }
+                row += 2 * N;
+            }
+        };
+        if (wave_live) {
+            const bool pk = ZR_DEC_PK && __builtin_amdgcn_readfirstlane(
+                                (uint32_t)(wave_all && (N & 3) == 0 && ((((uintptr_t)outb) & 3) == 0))) != 0;
+            if (pk) {
+                for (uint32_t t = 0; t < nfull; t++) {
+                    // the DMA of boundary t - 1; younger: tile t - 1's 4 packed stores
+                    if (t) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    refill();
+                    tile(t, true);
                 }
             } else {
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? eA >> 24 : eA), orsrc, voff, row, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? eB >> 24 : eB), orsrc, voff, row + N, 0);
+                for (uint32_t t = 0; t < nfull; t++) {
+                    if (t) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // (16 byte stores)
+                    refill();
+                    tile(t, false);
+                }
             }
-            row += 2 * N;
+            // ---- the last rows (<= TD steps): every chunk lands, one more request
+            // round (>= 48 bytes below y resident, a tail consumes <= 2 * TD)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            refill();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bad |= !(ABL & 4) && active && (int32_t)(p8 - yland8) < 0;
+            yland8 = ylo << 3;
+            uint32_t pos_snap = p8;
+            const uint64_t k0 = (uint64_t)nfull * TD;
+            const uint32_t nst = (uint32_t)(cmax - k0);
+            orsrc = byte_rsrc(outb + k0 * N);
+            for (uint32_t j = 0; j < nst; j++) {
+                const bool live = k0 + j < c;
+                uint32_t h, l, sf;
+                const uint32_t ent = step(readD(p8), h, l, sf);
+                p8 = p8 + 8 - sf;
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ent, orsrc, live ? voff : 0x80000000u,
+                                                     (uint32_t)(j * N), 0);
+                if (live) pos_snap = p8;
+            }
+            bad |= !(ABL & 4) && active && (int32_t)(pos_snap - yland8) < 0;
+            if (active) {
+                if (bad) {
+                    atomicAdd(&g_dec_fallbacks, 1ull);
+                    generic();
+                } else {
+                    // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
+                    const uint32_t consumed = ((YB << 3) - pos_snap) >> 3;
+                    if (consumed > L) set_invalid();
+                }
+            }
         }
-    };
-    uint32_t ppos8 = pos8 + TW * 8;  // wide shape: pos8 at the previous boundary (first: one byte a step)
+    } else {
+        const uintptr_t pend = sb + L;
+        const uintptr_t lo_lim = ((uintptr_t)e) & ~(uintptr_t)63;
+        auto clampa = [&](uintptr_t p) -> uintptr_t { return p > lo_lim ? p : lo_lim; };
+        uint32_t *lring = ring + tid;
+        // write the 64-B segment at absolute address g (64-aligned; cK = bytes g+16K..)
+        auto put_seg = [&](uint32_t g, const v4u c0, const v4u c1, const v4u c2, const v4u c3) __attribute__((always_inline)) {
+            const uint32_t r0 = ((g >> 2) + 1) & (RR - 1);  // 1 or 17
+            uint32_t *p = lring + r0 * FW;
+            p[0 * FW] = c0.x; p[1 * FW] = c0.y; p[2 * FW] = c0.z; p[3 * FW] = c0.w;
+            p[4 * FW] = c1.x; p[5 * FW] = c1.y; p[6 * FW] = c1.z; p[7 * FW] = c1.w;
+            p[8 * FW] = c2.x; p[9 * FW] = c2.y; p[10 * FW] = c2.z; p[11 * FW] = c2.w;
+            p[12 * FW] = c3.x; p[13 * FW] = c3.y; p[14 * FW] = c3.z;
+            if (MIR) p[15 * FW] = c3.w;             // row 16, or the mirror row 32
+            lring[((r0 + 15) & (RR - 1)) * FW] = c3.w;  // row 0 itself (r0 = 17; r0 = 1: row 16 again)
+        };
+        // prologue: the 64-B segment holding the last stream byte and the one below
+        const uintptr_t g1 = (pend - 1) & ~(uintptr_t)63;
+        {
+            // (addresses rebased on e: global loads, not flat)
+            const v4u *p1 = reinterpret_cast<const v4u *>(e + (int64_t)(clampa(g1) - (uintptr_t)e));
+            const v4u *p0 = reinterpret_cast<const v4u *>(e + (int64_t)(clampa(g1 - 64) - (uintptr_t)e));
+            const v4u a0 = p1[0], a1 = p1[1], a2 = p1[2], a3 = p1[3];
+            const v4u b0 = p0[0], b1 = p0[1], b2 = p0[2], b3 = p0[3];
+            put_seg((uint32_t)g1, a0, a1, a2, a3);
+            put_seg((uint32_t)(g1 - 64), b0, b1, b2, b3);
+        }
+        // positions are tracked as byte address * 8 (mod 2^32): the ring only needs the
+        // low bits and comparisons use 32-bit differences.
+        // PF (the 64-lane shape, one wave per SIMD, issue-bound): the lowest resident
+        // byte is kept as byte * 8 and as a signed offset from lo_lim (stream sets are
+        // < 2^31 bytes), so the refill address is one 32-bit max and one add, and the
+        // in-flight state is one flag per staging set. The 1024-lane shape keeps the
+        // 64-bit address and one (flag, tile) pair: measured 2.5 % faster there, the
+        // PF form 3.5 % faster at 64 lanes
+        constexpr bool PF = FW == 64;
+        uintptr_t lo64 = g1 - 64;                     // !PF: lowest resident byte
+        uint32_t lo8 = (uint32_t)(g1 - 64) << 3;      // PF: lowest resident byte * 8
+        int32_t lo = (int32_t)((g1 - 64) - lo_lim);  // PF: the same, from lo_lim (>= -64)
+        uint32_t pos8 = (uint32_t)pend << 3;  // bytes [.., pos) not yet consumed
+        uint32_t x = (uint32_t)X;
+        // D: the 4 stream bytes below p (byte p-1 on top)
+        auto readD = [&](uint32_t p8) -> uint32_t __attribute__((always_inline)) {
+            const uint32_t r = (p8 >> 5) & (RR - 1);
+            if constexpr (!MIR) {  // rows r and r + 1 (mod 32): byte offsets in the ring, the lane's column added
+                const uint32_t o0 = (p8 << 7) & ((RR - 1) * FW * 4), o1 = (o0 + FW * 4) & ((RR - 1) * FW * 4);
+                const char *base = reinterpret_cast<const char *>(ring) + tid * 4;
+                return __builtin_amdgcn_alignbit(*reinterpret_cast<const uint32_t *>(base + o1),
+                                                 *reinterpret_cast<const uint32_t *>(base + o0), p8);
+            }
+            const uint32_t *q = lring + r * FW;
+            return __builtin_amdgcn_alignbit(q[FW], q[0], p8);
+        };
+        // one decode step (rans.rs:472-507): renormalise from window D, decode, return
+        // the slot entry; hi/lo are the shifted (x : D) pair, sft = 8 + 8 * bytes consumed
+        auto step = [&](uint32_t D, uint32_t &hi, uint32_t &lo, uint32_t &sft) -> uint32_t __attribute__((always_inline)) {
+            sft = __builtin_clz(x) & 24;
+            const uint64_t t = ((((uint64_t)x) << 32) | D) << sft;
+            hi = (uint32_t)(t >> 32);
+            lo = (uint32_t)t;
+            if (WT && !(ABL & 2)) {  // 8-byte entry: x = f * (x >> 12) + (slot - start), sym in the top byte
+                const v2u e2 = *reinterpret_cast<const v2u *>(reinterpret_cast<const char *>(lds) + ((hi >> 5) & 0x7FF8));
+                x = __umul24(e2.x, hi >> 20) + e2.y;
+                return SH ? e2.x : e2.x >> 24;
+            }
+            const uint32_t ent = (ABL & 2) ? (hi & 0x0FFFFF00u) | 0x01000000u
+                                           : *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) +
+                                                                                 ((hi >> 6) & 0x3FFC));
+            x = __umul24(ent >> 20, hi >> 20) + ((ent >> 8) & 0xFFF);
+            // sensitivity probes (diagnostic builds): 16 = two more VALU on the step's
+            // chain, 32 = two more VALU off it
+            if (ABL & 16) asm volatile("v_add_u32 %0, 0, %0\n\tv_add_u32 %0, 0, %0" : "+v"(x));
+            if (ABL & 32) {
+                uint32_t d0, d1;
+                asm volatile("v_mov_b32 %0, 0\n\tv_mov_b32 %1, 1" : "=v"(d0), "=v"(d1));
+            }
+            return ent;
+        };
+        uint32_t sink = 0;
+        // staging registers of the segment loads issued at even / odd boundaries
+        v4u e0 = {0, 0, 0, 0}, e1 = e0, e2 = e0, e3 = e0, o0 = e0, o1 = e0, o2 = e0, o3 = e0;
+        bool pnd_e = false, pnd_o = false;  // PF: a segment in flight in the even / odd staging set
+        bool pnd = false;                   // !PF: a segment in flight, fetched at boundary ptile
+        uint32_t ptile = 0;
+        bool bad = false;
+        const uint64_t wbase = (uint64_t)blkF * FW + (tid & ~63u);
+        const bool wave_live = wbase < N;       // wave-uniform
+        const bool wave_all = wbase + 64 <= N;  // wave-uniform
+        uint8_t *outb = raw + a.raw_off[b] + (size_t)blkF * FW;
+        // output rows are addressed through a descriptor rebased every tile, so the
+        // 32-bit buffer offsets cover any buffer size. A lane without a stream
+        // stores at offset 2^31 (+ the row), beyond the descriptor's 2^31 - 1
+        // records: the hardware drops it, so the stores need no exec mask.
+        __amdgpu_buffer_rsrc_t orsrc = byte_rsrc(outb);
+        const uint32_t voff = active ? tid : 0x80000000u;
+        // packed stores (wide shape): lane 4q + r of a wave writes row r of streams
+        // 4q..4q+3; the transpose's byte selectors by the lane's place in its quad
+        const uint32_t voff_pk = (tid & ~3u) + (tid & 3u) * N;
+        const uint32_t psel1 = (tid & 2) ? 0x03020706u : 0x05040100u;  // 16-bit halves with lane ^ 2
+        const uint32_t psel2 = (tid & 1) ? 0x03070105u : 0x06020400u;  // bytes with lane ^ 1
+        // PF: DT2-step tiles with k0 + DT2 < cmax. Wide shape: TW-step tiles over
+        // the rows every stream of the buffer has (n / N of them), the rest in the
+        // tail loop
+        constexpr uint32_t TW = 32;
+        const uint32_t nfull = PF ? (uint32_t)((cmax - 1) / DT2) : (uint32_t)((n / N) / TW);
+        auto lov8 = [&]() -> uint32_t { return PF ? lo8 : (uint32_t)lo64 << 3; };
+        // a segment lands: the staging set becomes the 64 bytes below the resident ones
+        auto land = [&](const v4u c0, const v4u c1, const v4u c2, const v4u c3) __attribute__((always_inline)) {
+            if constexpr (PF) {
+                lo8 -= 512;
+                lo -= 64;
+                put_seg(lo8 >> 3, c0, c1, c2, c3);
+            } else {
+                lo64 -= 64;
+                if (!(ABL & 64)) put_seg((uint32_t)lo64, c0, c1, c2, c3);
+            }
+        };
+
+        // lanes that fetch nothing at a boundary load a line of the table instead
+        // (L2-resident, one request per wave; a lane-private re-load measured 2x
+        // slower at 1024 lanes per CU): the loads are issued unconditionally so
+        // that no control flow ever merges a staging register still in flight
+        const uintptr_t dummy = (uintptr_t)T->slot + 64 * (tid >> 6);
+
+        // tile boundary t, staging set (s0..s3) = the set of parity t & 1, pmine its
+        // in-flight flag
+        auto boundary = [&](uint32_t t, v4u &s0, v4u &s1, v4u &s2, v4u &s3, bool &pmine, bool pother) __attribute__((always_inline)) {
+            // every read of the previous tile was at or above pos - 4 (the no-refill
+            // ablation reads stale ring bytes on purpose: no fallback there)
+            bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+            if (t >= 2) {
+                // wait for the loads of boundary t-2: younger are the 16 stores of tile
+                // t-2, the 4 loads of boundary t-1 and the 16 stores of tile t-1 (every
+                // wave issues all of them: lanes without a stream store out of range)
+                if (ABL & 1)
+                    asm volatile("s_waitcnt vmcnt(4)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(36)" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)::"memory");
+                if (PF ? pmine : pnd && ptile + 2 == t) {  // the segment this set fetched at boundary t - 2
+                    land(s0, s1, s2, s3);
+                    pmine = pnd = false;
+                }
+            }
+            // a lane with <= 64 unread resident bytes fetches the segment below
+            const bool issue =
+                !(ABL & 4) && active && (PF ? !pmine && !pother : !pnd) && (int32_t)(pos8 - lov8()) <= 64 * 8;
+            const uintptr_t g = !issue ? dummy : PF ? lo_lim + (uint32_t)max(lo - 64, 0) : clampa(lo64 - 64);
+            asm_load16(s0, g);
+            asm_load16_off<16>(s1, g);
+            asm_load16_off<32>(s2, g);
+            asm_load16_off<48>(s3, g);
+            if constexpr (PF) {
+                pmine = pmine || issue;
+            } else if (issue) {
+                pnd = true;
+                ptile = t;
+            }
+        };
+        // DT2 steps in pairs; one ring read per pair
+        auto tile = [&](uint32_t t) __attribute__((always_inline)) {
+            uint32_t D = readD(pos8);
+            orsrc = byte_rsrc(outb + (uint64_t)t * DT2 * N);
+            uint32_t row = 0;
+    #pragma unroll
+            for (int j = 0; j < DT2 / 2; j++) {
+                uint32_t hA, lA, sA, hB, lB, sB;
+                const uint32_t eA = step(D, hA, lA, sA);
+                const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
+                uint32_t used;  // sA + sB - 16 = 8 * bytes consumed by the pair
+                asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
+                pos8 -= used;
+                if (j + 1 < DT2 / 2) D = readD(pos8);
+                if (ABL & 1) {
+                    sink += eA ^ eB;
+                } else {  // no exec mask: a lane without a stream stores out of range (dropped)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eA, orsrc, voff, row, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)eB, orsrc, voff, row + N, 0);
+                }
+                row += 2 * N;
+            }
+        };
+
+        // ---- wide shape (1024 lanes per CU, 4 waves per SIMD): TW = 32-step tiles;
+        // a refill issued at boundary t lands at boundary t + 1 (32 steps, a few us,
+        // cover the load: one staging set, half the boundaries of 16-step tiles).
+        // Full waves over 4-aligned output pack the bytes of 4 steps into one dword
+        // store per lane: the quad's 4 x 4 bytes (lane r of the quad holds rows
+        // 4g..4g+3 of its stream) are transposed by two DPP lane swaps + v_perm,
+        // so lane 4q + r stores row 4g + r of streams 4q..4q+3: 8 dword stores per
+        // tile instead of 32 byte stores.
+        auto tile_w = [&](uint32_t t, bool pk) __attribute__((always_inline)) {
+            uint32_t D = readD(pos8);
+            orsrc = byte_rsrc(outb + ((ABL & 256) ? 0 : (uint64_t)t * TW * N));
+            uint32_t row = 0, pk0 = 0;
+    #pragma unroll
+            for (int j = 0; j < (int)TW / 2; j++) {
+                uint32_t hA, lA, sA, hB, lB, sB;
+                const uint32_t eA = step(D, hA, lA, sA);
+                const uint32_t eB = step(__builtin_amdgcn_alignbyte(hA, lA, 1), hB, lB, sB);
+                uint32_t used;
+                asm("v_add3_u32 %0, %1, %2, -16" : "=v"(used) : "v"(sA), "v"(sB));
+                pos8 -= used;
+                if (j + 1 < (int)TW / 2) D = readD(pos8);
+                if (ABL & 1) {
+                    sink += eA ^ eB;
+                } else if (pk) {
+                    // (SH: the symbols are the entries' top bytes)
+                    if ((j & 1) == 0) {
+                        pk0 = __builtin_amdgcn_perm(eB, eA, SH ? 0x0c0c0703u : 0x0c0c0400u);  // [eA, eB, 0, 0]
+                    } else {
+                        uint32_t q = __builtin_amdgcn_perm(eB, eA, SH ? 0x07030c0cu : 0x04000c0cu) | pk0;  // rows 4g..4g+3
+                        uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0x4E, 0xF, 0xF, false);  // lane ^ 2
+                        q = __builtin_amdgcn_perm(x, q, psel1);
+                        x = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+                        q = __builtin_amdgcn_perm(x, q, psel2);
+                        __builtin_amdgcn_raw_buffer_store_b32(q, orsrc, voff_pk, (ABL & 256) ? 0 : row - 2 * N, 0);
+                    }
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? eA >> 24 : eA), orsrc, voff, row, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? eB >> 24 : eB), orsrc, voff, row + N, 0);
+                }
+                row += 2 * N;
+            }
+        };
+        uint32_t ppos8 = pos8 + TW * 8;  // wide shape: pos8 at the previous boundary (first: one byte a step)
 #ifndef ZR_DEC_PAIR
 #define ZR_DEC_PAIR 1
 #endif
-    // PAIR: a refill that starts a 128-B line (the segment below lo64 is the
-    // line's upper half) loads the lower half too, into the second staging set
-    // (o), which lands from registers at a later boundary: both halves of every
-    // line are requested together, instead of the lower half 64 steps later,
-    // when the L2 has usually evicted the line (the decoder's FETCH_SIZE was
-    // 1.83x its stream bytes)
-    constexpr bool PAIR = ZR_DEC_PAIR && !PF;
-    bool hasB = false;  // PAIR: o holds the segment below e's, loaded, not yet landed
-    auto boundary_w = [&](uint32_t t, bool pk) __attribute__((always_inline)) {
-        bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
-        if (t >= 1) {
-            // the loads of boundary t - 1; younger: tile t-1's stores
-            if (ABL & 512)
-                asm volatile("" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1), "+v"(o2),
-                             "+v"(o3)::"memory");
-            else if (ABL & 1)
-                asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
-                             "+v"(o2), "+v"(o3)::"memory");
-            else if (pk)
-                asm volatile("s_waitcnt vmcnt(8)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
-                             "+v"(o2), "+v"(o3)::"memory");
-            else
-                asm volatile("s_waitcnt vmcnt(32)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
-                             "+v"(o2), "+v"(o3)::"memory");
-            // the segment lands once every byte of the ring rows it takes is
-            // consumed; otherwise the load below fetches it again
-            // (flags updated outside the branches: stores to either of two
-            // flags in two branches were merged into one store through a
-            // selected address, which put both flags in scratch memory)
-            const bool landable = (int32_t)(pos8 - lov8()) <= 64 * 8;
-            const bool lE = pnd && landable, lO = PAIR && !pnd && hasB && landable;
-            if (lE) land(e0, e1, e2, e3);
-            if (lO) land(o0, o1, o2, o3);
-            pnd = pnd && !lE;
-            hasB = hasB && !lO;
-        }
-        // issue when the lane will have consumed the rows by the next boundary,
-        // predicting that the next tile consumes what the last one did (a one-tile
-        // lag with the 16-step tiles' "<= 64 unread" rule left 0-32 bytes at the
-        // landing and sent most lanes to the generic decoder). A lane whose o
-        // still holds the next segment issues nothing new. A segment that did not
-        // land is fetched again whether or not the prediction still asks for it:
-        // dropping it while o holds the one below would land o in its place.
-        const uint32_t used8 = ppos8 - pos8;
-        ppos8 = pos8;
-        const bool need = !(ABL & 4) && active && (int32_t)(pos8 - used8 - lov8()) <= 64 * 8;
-        const bool issue = pnd || (need && !hasB);
-        const uintptr_t g = (!issue || (ABL & 128)) ? dummy : clampa(lo64 - 64);
-        asm_load16(e0, g);
-        asm_load16_off<16>(e1, g);
-        asm_load16_off<32>(e2, g);
-        asm_load16_off<48>(e3, g);
-        if constexpr (PAIR) {
-            const bool pair = issue && !pnd && !hasB && (lo64 & 127) == 0 && lo64 - 128 >= lo_lim && !(ABL & 128);
-            if (pair) {  // (tied operands: the phi at the merge keeps o in place)
-                const uintptr_t gb = lo64 - 128;
-                asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(o0) : "v"(gb) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "+v"(o1) : "v"(gb) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "+v"(o2) : "v"(gb) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off offset:48" : "+v"(o3) : "v"(gb) : "memory");
+        // PAIR: a refill that starts a 128-B line (the segment below lo64 is the
+        // line's upper half) loads the lower half too, into the second staging set
+        // (o), which lands from registers at a later boundary: both halves of every
+        // line are requested together, instead of the lower half 64 steps later,
+        // when the L2 has usually evicted the line (the decoder's FETCH_SIZE was
+        // 1.83x its stream bytes)
+        constexpr bool PAIR = ZR_DEC_PAIR && !PF;
+        bool hasB = false;  // PAIR: o holds the segment below e's, loaded, not yet landed
+        auto boundary_w = [&](uint32_t t, bool pk) __attribute__((always_inline)) {
+            bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+            if (t >= 1) {
+                // the loads of boundary t - 1; younger: tile t-1's stores
+                if (ABL & 512)
+                    asm volatile("" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1), "+v"(o2),
+                                 "+v"(o3)::"memory");
+                else if (ABL & 1)
+                    asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
+                                 "+v"(o2), "+v"(o3)::"memory");
+                else if (pk)
+                    asm volatile("s_waitcnt vmcnt(8)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
+                                 "+v"(o2), "+v"(o3)::"memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(32)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
+                                 "+v"(o2), "+v"(o3)::"memory");
+                // the segment lands once every byte of the ring rows it takes is
+                // consumed; otherwise the load below fetches it again
+                // (flags updated outside the branches: stores to either of two
+                // flags in two branches were merged into one store through a
+                // selected address, which put both flags in scratch memory)
+                const bool landable = (int32_t)(pos8 - lov8()) <= 64 * 8;
+                const bool lE = pnd && landable, lO = PAIR && !pnd && hasB && landable;
+                if (lE) land(e0, e1, e2, e3);
+                if (lO) land(o0, o1, o2, o3);
+                pnd = pnd && !lE;
+                hasB = hasB && !lO;
             }
-            hasB = hasB || pair;
-        }
-        pnd = issue;
-    };
-    if (!PF && wave_live) {
-        // packed stores: every lane of the wave a stream, 4-aligned rows
-#ifndef ZR_DEC_PK
-#define ZR_DEC_PK 1
-#endif
-        const bool pk = ZR_DEC_PK && __builtin_amdgcn_readfirstlane(
-                            (uint32_t)(wave_all && (N & 3) == 0 && ((((uintptr_t)outb) & 3) == 0))) != 0;
-        if (pk) {
-            for (uint32_t t = 0; t < nfull; t++) {
-                if (!(ABL & 1024)) boundary_w(t, true);
-                tile_w(t, true);
+            // issue when the lane will have consumed the rows by the next boundary,
+            // predicting that the next tile consumes what the last one did (a one-tile
+            // lag with the 16-step tiles' "<= 64 unread" rule left 0-32 bytes at the
+            // landing and sent most lanes to the generic decoder). A lane whose o
+            // still holds the next segment issues nothing new. A segment that did not
+            // land is fetched again whether or not the prediction still asks for it:
+            // dropping it while o holds the one below would land o in its place.
+            const uint32_t used8 = ppos8 - pos8;
+            ppos8 = pos8;
+            const bool need = !(ABL & 4) && active && (int32_t)(pos8 - used8 - lov8()) <= 64 * 8;
+            const bool issue = pnd || (need && !hasB);
+            const uintptr_t g = (!issue || (ABL & 128)) ? dummy : clampa(lo64 - 64);
+            asm_load16(e0, g);
+            asm_load16_off<16>(e1, g);
+            asm_load16_off<32>(e2, g);
+            asm_load16_off<48>(e3, g);
+            if constexpr (PAIR) {
+                const bool pair = issue && !pnd && !hasB && (lo64 & 127) == 0 && lo64 - 128 >= lo_lim && !(ABL & 128);
+                if (pair) {  // (tied operands: the phi at the merge keeps o in place)
+                    const uintptr_t gb = lo64 - 128;
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(o0) : "v"(gb) : "memory");
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "+v"(o1) : "v"(gb) : "memory");
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "+v"(o2) : "v"(gb) : "memory");
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:48" : "+v"(o3) : "v"(gb) : "memory");
+                }
+                hasB = hasB || pair;
             }
-        } else {
-            for (uint32_t t = 0; t < nfull; t++) {
-                boundary_w(t, false);
-                tile_w(t, false);
-            }
-        }
-    }
-    if (wave_live) {
-        if constexpr (PF) {
-            for (uint32_t t = 0; t < nfull; t += 2) {
-                boundary(t, e0, e1, e2, e3, pnd_e, pnd_o);
-                tile(t);
-                if (t + 1 < nfull) {
-                    boundary(t + 1, o0, o1, o2, o3, pnd_o, pnd_e);
-                    tile(t + 1);
+            pnd = issue;
+        };
+        if (!PF && wave_live) {
+            // packed stores: every lane of the wave a stream, 4-aligned rows
+            const bool pk = ZR_DEC_PK && __builtin_amdgcn_readfirstlane(
+                                (uint32_t)(wave_all && (N & 3) == 0 && ((((uintptr_t)outb) & 3) == 0))) != 0;
+            if (pk) {
+                for (uint32_t t = 0; t < nfull; t++) {
+                    if (!(ABL & 1024)) boundary_w(t, true);
+                    tile_w(t, true);
+                }
+            } else {
+                for (uint32_t t = 0; t < nfull; t++) {
+                    boundary_w(t, false);
+                    tile_w(t, false);
                 }
             }
         }
-        // ---- last tile (1..DT2 steps): every segment in flight lands first
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
-                     "+v"(o2), "+v"(o3)::"memory");
-        bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
-        if constexpr (PF) {
-            if (pnd_o) land(o0, o1, o2, o3);
-            if (pnd_e) land(e0, e1, e2, e3);
-        } else {  // (wide shape: e, then PAIR's o)
-            const bool lE = pnd && (int32_t)(pos8 - lov8()) <= 64 * 8;
-            if (lE) land(e0, e1, e2, e3);
-            if (PAIR && !(pnd && !lE) && hasB && (int32_t)(pos8 - lov8()) <= 64 * 8) land(o0, o1, o2, o3);
-        }
-        uint32_t pos_snap = pos8;
-        const uint64_t k0 = (uint64_t)nfull * (PF ? DT2 : TW);
-        const uint32_t nst = (uint32_t)(cmax - k0);
-        orsrc = byte_rsrc(outb + k0 * N);
-        for (uint32_t j = 0; j < nst; j++) {
-            const uint64_t k = k0 + j;
-            const bool live = k < c;
-            if (live) bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
-            uint32_t h, l, sf;
-            const uint32_t ent = step(readD(pos8), h, l, sf);
-            pos8 = pos8 + 8 - sf;
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? ent >> 24 : ent), orsrc, live ? voff : 0x80000000u,
-                                                 (uint32_t)(j * N), 0);
-            if (live) pos_snap = pos8;
-        }
-        if ((ABL & 1) && sink == 0x9E3779B9u) a.status[b] = 7;  // keeps the ablated work live
-        if ((ABL & 8) && tid == 0) {
-            uint64_t *r = reinterpret_cast<uint64_t *>(w.scratch) + 4 * (size_t)blockIdx.x;
-            r[0] = dbg_t0;
-            r[1] = __builtin_amdgcn_s_memrealtime();
-            r[2] = __builtin_amdgcn_s_memtime() - dbg_c0;
-            r[3] = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) | ((uint64_t)__builtin_amdgcn_s_getreg(0xF814) << 32);
-        }
-        if (active) {
-            if (bad) {
-                atomicAdd(&g_dec_fallbacks, 1ull);
-                generic();
-            } else {
-                // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
-                const uint32_t consumed = (((uint32_t)pend << 3) - pos_snap) >> 3;
-                if (consumed > L) set_invalid();
+        if (wave_live) {
+            if constexpr (PF) {
+                for (uint32_t t = 0; t < nfull; t += 2) {
+                    boundary(t, e0, e1, e2, e3, pnd_e, pnd_o);
+                    tile(t);
+                    if (t + 1 < nfull) {
+                        boundary(t + 1, o0, o1, o2, o3, pnd_o, pnd_e);
+                        tile(t + 1);
+                    }
+                }
+            }
+            // ---- last tile (1..DT2 steps): every segment in flight lands first
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(o0), "+v"(o1),
+                         "+v"(o2), "+v"(o3)::"memory");
+            bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+            if constexpr (PF) {
+                if (pnd_o) land(o0, o1, o2, o3);
+                if (pnd_e) land(e0, e1, e2, e3);
+            } else {  // (wide shape: e, then PAIR's o)
+                const bool lE = pnd && (int32_t)(pos8 - lov8()) <= 64 * 8;
+                if (lE) land(e0, e1, e2, e3);
+                if (PAIR && !(pnd && !lE) && hasB && (int32_t)(pos8 - lov8()) <= 64 * 8) land(o0, o1, o2, o3);
+            }
+            uint32_t pos_snap = pos8;
+            const uint64_t k0 = (uint64_t)nfull * (PF ? DT2 : TW);
+            const uint32_t nst = (uint32_t)(cmax - k0);
+            orsrc = byte_rsrc(outb + k0 * N);
+            for (uint32_t j = 0; j < nst; j++) {
+                const uint64_t k = k0 + j;
+                const bool live = k < c;
+                if (live) bad |= !(ABL & (4 | 64 | 128 | 1024)) && active && (int32_t)(pos8 - 32 - lov8()) < 0;
+                uint32_t h, l, sf;
+                const uint32_t ent = step(readD(pos8), h, l, sf);
+                pos8 = pos8 + 8 - sf;
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(SH ? ent >> 24 : ent), orsrc, live ? voff : 0x80000000u,
+                                                     (uint32_t)(j * N), 0);
+                if (live) pos_snap = pos8;
+            }
+            if ((ABL & 1) && sink == 0x9E3779B9u) a.status[b] = 7;  // keeps the ablated work live
+            if ((ABL & 8) && tid == 0) {
+                uint64_t *r = reinterpret_cast<uint64_t *>(w.scratch) + 4 * (size_t)blockIdx.x;
+                r[0] = dbg_t0;
+                r[1] = __builtin_amdgcn_s_memrealtime();
+                r[2] = __builtin_amdgcn_s_memtime() - dbg_c0;
+                r[3] = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) | ((uint64_t)__builtin_amdgcn_s_getreg(0xF814) << 32);
+            }
+            if (active) {
+                if (bad) {
+                    atomicAdd(&g_dec_fallbacks, 1ull);
+                    generic();
+                } else {
+                    // bytes consumed by renormalisation (rans.rs:480-482 "Insufficient data")
+                    const uint32_t consumed = (((uint32_t)pend << 3) - pos_snap) >> 3;
+                    if (consumed > L) set_invalid();
+                }
             }
         }
     }
     finish();
+}
+
+template <int FW, int ABL, bool WT = false>
+__global__ __launch_bounds__(FW) void k_dec_xn_fast(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
+                                                   uint32_t nblkF, uint64_t epoch) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[dec_lds_words<FW, WT, 0>()];
+    dec_xn_body<FW, ABL, WT, 0>(enc, raw, a, w, nblkF, epoch, lds);
+}
+
+// the 8-waves-per-SIMD decoder: 1024-lane workgroups with 80 KiB of LDS (16 KiB
+// slot table + the 64 KiB DMA ring), two per CU, <= 64 VGPRs (opt-in,
+// zr_rans_set_decoder_ring(2)): built for batches of >= 2^19 streams (2048 per
+// CU); measured slower than k_dec_xn_fast at every N
+template <int ABL>
+__global__ __launch_bounds__(1024, 8) void k_dec_xn_dma(const uint8_t *enc, uint8_t *raw, KArgs a, RansWork w,
+                                                        uint32_t nblkF, uint64_t epoch) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[dec_lds_words<1024, false, 1>()];
+    dec_xn_body<1024, ABL, false, 1>(enc, raw, a, w, nblkF, epoch, lds);
 }
 
 __global__ __launch_bounds__(64) void k_dec_x1_generic(const uint8_t *enc, uint8_t *raw, KArgs a) {
@@ -3415,6 +3627,19 @@ int32_t zr_rans_set_encoder_width(uint32_t lanes) {
     return ZR_OK;
 }
 
+int32_t zr_rans_set_decoder_ring(int32_t ring) {
+    clear_error();
+    if (ring < 0 || ring > 2) return set_error(ZR_INVALID_INPUT, "decoder ring must be 0 (auto), 1 or 2");
+    g_dec_ring.store(ring, std::memory_order_relaxed);
+    return ZR_OK;
+}
+
+const char *zr_rans_decoder_kernel(uint32_t n_buffers, uint32_t n_streams) {
+    if (n_streams <= 1) return "k_dec_x1_fast";
+    if ((uint64_t)n_buffers * n_streams <= (1u << 16)) return "k_dec_xn_fast";  // (one-wave workgroups)
+    return dec_uses_dma(n_buffers, n_streams) ? "k_dec_xn_dma" : "k_dec_xn_fast";
+}
+
 int32_t zr_rans_set_encode_split(int32_t quarters) {
     clear_error();
     if (quarters < 0 || quarters > 3) return set_error(ZR_INVALID_INPUT, "encode split must be 0..3 quarters");
@@ -3721,6 +3946,18 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
             else
                 launch_timed("rans_decode", k_dec_xn_fast<64, 0, false>, dim3(nblkF * a.B), dim3(64), 0, s, enc, raw,
                              a, w, nblkF, epoch);
+        } else if (dec_uses_dma(a.B, a.N)) {
+            // (N >= 64: the header below a buffer's first stream is >= 768 bytes,
+            // more than a lane's chunk requests reach below its stream)
+            const uint32_t nblkF = (uint32_t)ceil_div(a.N, 1024);
+#ifdef ZR_DIAG
+            static const int abl = getenv("ZR_DEC_ABL") ? atoi(getenv("ZR_DEC_ABL")) : 0;  // profiling only
+            auto kern = abl == 1 ? k_dec_xn_dma<1> : abl == 4 ? k_dec_xn_dma<4> : abl == 5 ? k_dec_xn_dma<5>
+                                                                                             : k_dec_xn_dma<0>;
+#else
+            auto kern = k_dec_xn_dma<0>;
+#endif
+            launch_timed("rans_decode", kern, dim3(nblkF * a.B), dim3(1024), 0, s, enc, raw, a, w, nblkF, epoch);
         } else {
             const uint32_t nblkF = (uint32_t)ceil_div(a.N, 1024);
 #ifdef ZR_DIAG
