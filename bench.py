@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--dec-ring", type=int, default=0, choices=[0, 1, 2],
                    help="rans: the xN decoder's ring (zr_rans_set_decoder_ring): 0 auto, 1 VGPR-staged "
                         "(k_dec_xn_fast), 2 LDS-DMA chunks (k_dec_xn_dma, 8 waves per SIMD)")
+    p.add_argument("--enc-fused", type=int, default=None, choices=[0, 1],
+                   help="rans: encode + compaction in one launch with look-back (zr_rans_set_encode_fused; "
+                        "default: the library's)")
     p.add_argument("--enc-split", type=int, default=None, choices=[0, 1, 2, 3],
                    help="rans: encode a wide batch in two parts (the first q/4 of the buffers, then the rest), "
                         "the second part's encoder and the first part's compaction in one dispatch "
@@ -847,6 +850,12 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     syms = dict(RANS_SYMS)  # the decode kernel this batch ran (zr_rans_decoder_kernel)
     if hasattr(L, "zr_rans_decoder_kernel"):
         syms["rans_decode"] = L.zr_rans_decoder_kernel(B, N).decode()
+    # encode + compaction in one launch (k_enc_lb): no separate compaction ran; its
+    # roofline counts the encode's algorithmic bytes (N_in + C) over the fused time
+    fused = (hasattr(L, "zr_rans_get_encode_fused") and L.zr_rans_get_encode_fused() == 1
+             and kms.get("rans_compact", 0) == 0 and not split)
+    if fused:
+        syms["rans_encode"] = "k_enc_lb"
     rans_bytes = {"rans_encode": total + comp_bytes, "rans_decode": comp_bytes + total,
                   "rans_compact": 2 * comp_bytes, "histogram": total}
     if split:
@@ -885,6 +894,9 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
                    **({"encode_schedule": f"split at buffer {h}: encoder(0..{h}) -> encoder({h}..{B}) + "
                                           f"compaction(0..{h}) in one dispatch -> compaction({h}..{B})"}
                       if split else {}),
+                   **({"encode_schedule": "encode + compaction in one launch (k_enc_lb: each encoder workgroup "
+                                          "compacts its own streams after a look-back on its buffer's block sums)"}
+                      if fused else {}),
                    **({"pipelined": "two distinct 256 MiB batches alternate; step k codes one batch (encode -> "
                                     "decode) while the histogram + table of the other run on a second HIP stream"}
                       if pipe else {})},
@@ -1074,6 +1086,8 @@ def main():
         raise SystemExit(f"encoder width {args.enc_width} refused")
     if args.dec_ring and L.zr_rans_set_decoder_ring(args.dec_ring):
         raise SystemExit(f"decoder ring {args.dec_ring} refused")
+    if args.enc_fused is not None and L.zr_rans_set_encode_fused(args.enc_fused):
+        raise SystemExit(f"encode fused {args.enc_fused} refused")
     if args.enc_split is not None and L.zr_rans_set_encode_split(args.enc_split):
         raise SystemExit(f"encode split {args.enc_split} refused")
 

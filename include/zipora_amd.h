@@ -176,6 +176,14 @@ int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *batc
  * measured slower. Both decode the same format
  * bit for bit (rans.rs:555-651). */
 int32_t zr_rans_set_decoder_ring(int32_t ring);
+/* Tuning (no reference counterpart): encode and stream compaction in one
+ * launch, process-wide (1 on, 0 off): every 256-stream encoder workgroup
+ * compacts its own streams after a look-back on the byte sums of its buffer's
+ * lower blocks (the same reference layout, rans.rs:402-419). Applies to
+ * batches of > 2^16 streams of short streams (<= 64 blocks of 256 streams per
+ * buffer, <= ~1.2 KiB of output per stream), not under graph capture. */
+int32_t zr_rans_set_encode_fused(int32_t on);
+int32_t zr_rans_get_encode_fused(void);
 /* The name of the xN decode kernel a batch of n_buffers x n_streams (every
  * buffer at least n_streams bytes) runs under the current setting (reports and
  * profiles; a static string). */

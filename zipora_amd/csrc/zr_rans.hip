@@ -173,7 +173,6 @@ __device__ __forceinline__ void hist_tab_tail(uint32_t *hist, RansDTab *tab, uin
     if (threadIdx.x == 0) last = tab_arrive(epoch, blockIdx.x, gridDim.x) ? 1u : 0u;
     __syncthreads();
     if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's adds before the exchange
     const uint32_t f = __hip_atomic_exchange(&hist[threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tab_build(f, tab, h);
 }
@@ -431,12 +430,18 @@ __device__ unsigned int g_tab_tick[TT_SLOTS][9];
 __device__ __noinline__ bool tab_arrive(uint64_t epoch, uint32_t g, uint32_t nwg) {
     unsigned int *const t = g_tab_tick[epoch % TT_SLOTS];
     const uint32_t sh = g & 7, in_sh = (nwg - sh + 7) / 8, nsh = min(nwg, 8u);
-    // release: this workgroup's histogram adds (performed: vmcnt(0) before the
-    // call) are ordered before its ticket; acq_rel at the top counter chains
-    // the shards' releases to the last workgroup, which acquires (hist_tab_tail)
-    if (__hip_atomic_fetch_add(&t[sh], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) + 1 != in_sh) return false;
+    // Ordering: the histogram adds, the tickets and the last
+    // workgroup's exchange are all agent-scope atomics, performed at the one
+    // point of coherence of these words (not in a non-coherent L2), and every
+    // workgroup's adds are complete (vmcnt(0), which retires a no-return atomic
+    // only once it is performed) before its ticket is taken, so the last
+    // ticket's exchange reads every count. No plain store is published, so no
+    // release/acquire fence is needed; the formal pair (a release fetch_add per
+    // workgroup, an acquire in the last) measured +27 us on k_hist (0.065 ->
+    // 0.092 ms, round 5: an L2 write-back per workgroup) and was removed
+    if (__hip_atomic_fetch_add(&t[sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 != in_sh) return false;
     __hip_atomic_store(&t[sh], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_fetch_add(&t[8], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 != nsh) return false;
+    if (__hip_atomic_fetch_add(&t[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 != nsh) return false;
     __hip_atomic_store(&t[8], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
 }
@@ -517,6 +522,12 @@ static bool dec_uses_dma(uint32_t B, uint32_t N) {
 // encoder(lower half) -> encoder(upper half) + compaction(lower half) in one
 // dispatch (k_enc_cmp_fused) -> compaction(upper half)
 static std::atomic<int> g_enc_split{ZR_ENC_SPLIT_DEFAULT};
+// encode + compaction in one launch with look-back (k_enc_lb): 0 off, 1 on
+// (zr_rans_set_encode_fused) where the batch qualifies
+#ifndef ZR_ENC_FUSED_DEFAULT
+#define ZR_ENC_FUSED_DEFAULT 0
+#endif
+static std::atomic<int> g_enc_fused{ZR_ENC_FUSED_DEFAULT};
 #ifndef ZR_ENC_PF
 #define ZR_ENC_PF 1
 #endif
@@ -595,9 +606,12 @@ constexpr uint32_t enc_xn_lds_bytes() {
 }
 // the encoder of workgroup vblk (its blockIdx.x in k_enc_xn; k_enc_cmp_fused
 // runs it beside the compaction of other buffers), LDS from the caller
+// lbtag (non-zero: k_enc_lb): the block sum is published with the call's tag in
+// bits 40..62 by an agent-scope atomic store, for the look-back of the
+// workgroups of the buffer's higher blocks
 template <uint32_t EW, int ABL, bool IL>
 __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, const RansWork &w, uint32_t vblk,
-                                            uint8_t *const lds) {
+                                            uint8_t *const lds, uint64_t lbtag = 0) {
     // DB: two input tiles, written alternately, so one barrier per tile
     // separates a tile's writes from its reads (the other barrier kept the
     // next tile's writes from overtaking slow readers); the room comes from a
@@ -1029,8 +1043,14 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
         // the compaction uses this only for buffers below 4 GiB)
         if (active) w.st_off[(size_t)b * N + s] = (uint32_t)(ex & ((1ull << 55) - 1));
         const uint32_t blk256 = (blk * EW + tid) / 256;
-        if ((tid & 255) == 0 && blk256 < w.nblk)
-            w.blocksum[(size_t)b * w.nblk + blk256] = (r & ((1ull << 55) - 1)) | ((r >> 55) ? BS_ERR : 0);
+        if ((tid & 255) == 0 && blk256 < w.nblk) {
+            const uint64_t bs = (r & ((1ull << 55) - 1)) | ((r >> 55) ? BS_ERR : 0);
+            if (lbtag)
+                __hip_atomic_store(reinterpret_cast<unsigned long long *>(&w.blocksum[(size_t)b * w.nblk + blk256]),
+                                   (unsigned long long)(bs | (lbtag << 40)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                w.blocksum[(size_t)b * w.nblk + blk256] = bs;
+        }
     } else {  // narrow workgroups add their wave sums into the zeroed block sum
         const uint64_t ws = wave_sum(active ? bytes : 0);
         const bool wbad = __any(bad);
@@ -1162,9 +1182,15 @@ struct CmpLds {
     int ilm[CS][4];  // IL, per stream in the window: quad rows [x, y), image bytes [z, w) (z: its quad 0)
     __attribute__((aligned(16))) uint8_t img[CWIN];
 };
-template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0>  // streams per group (divides 64), window bytes, loads in flight
+// LB (k_enc_lb): the block sums are published by the encoder workgroups of the
+// same launch with the call's tag (lbtag, bits 40..62); a group polls until the
+// sums it needs carry it: the buffer's blocks below its own and its own (all of
+// them for the status writer, group 0 of the buffer's LAST block, whose blocks
+// all took lower tickets). Flags are checked over the same blocks.
+constexpr uint64_t LB_SUM = (1ull << 40) - 1, LB_TAGM = (1ull << 23) - 1;
+template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0, bool LB = false>  // streams per group (divides 64), window bytes, loads in flight
 __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const RansWork &w, uint32_t nwin,
-                                             int has_off, uint32_t vblk, uint8_t *const smem) {
+                                             int has_off, uint32_t vblk, uint8_t *const smem, uint64_t lbtag = 0) {
     static_assert(CS <= 64 && 64 % CS == 0, "a group's streams are lanes of one wave");
     CmpLds<CS, CWIN> &S = *reinterpret_cast<CmpLds<CS, CWIN> *>(smem);
     auto &sh = S.sh;
@@ -1278,16 +1304,34 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
             // every load of the setup issued at once (one memory round trip): the
             // block sums, and the group's lengths, offsets and (first window)
             // final states, used only if no block is flagged
-            const uint64_t v = lane < nblk ? w.blocksum[(size_t)b * nblk + lane] : 0;
+            const bool writer = LB ? blk == nblk - 1 && grp % gpb == 0 && wi == 0 : grp == 0 && wi == 0;
+            uint64_t v = !LB && lane < nblk ? w.blocksum[(size_t)b * nblk + lane] : 0;
             const bool mine = lane < ns;
             const uint32_t sb = s0 + lane;
             const uint32_t L = mine ? w.st_len[(size_t)b * N + sb] : 0;
             const uint32_t o32 = mine ? w.st_off[(size_t)b * N + sb] : 0;
             const uint32_t X = mine && wi == 0 ? w.st_state[(size_t)b * N + sb] : 0;
+            if constexpr (LB) {
+                const uint32_t nchk = writer ? nblk : blk + 1;
+                unsigned long long *const bsp =
+                    reinterpret_cast<unsigned long long *>(&w.blocksum[(size_t)b * nblk + min(lane, nblk - 1)]);
+                // (every block taking part has a lower ticket: it is running or done. A
+                // bound on the wait all the same: a hang would cost the whole GPU)
+                for (uint32_t it = 0;; it++) {
+                    v = __hip_atomic_load(bsp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(lane >= nchk || ((v >> 40) & LB_TAGM) == lbtag)) break;
+                    if (it >= (1u << 22)) {  // (never seen) report the buffer invalid
+                        v = BS_ERR;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+                v = lane < nchk ? (v & (LB_SUM | BS_ERR)) : 0;
+            }
             const uint64_t c = v & ~BS_ERR;
             const uint64_t below = wave_sum(lane < blk ? c : 0);
             const bool flagged = __any((v >> 63) != 0);
-            if (grp == 0 && wi == 0) {
+            if (writer) {
                 const uint64_t tot = wave_sum(c);
                 if (lane == 0) {
                     a.enc_len[b] = (uint64_t)N * 12 + tot;
@@ -1527,6 +1571,45 @@ __global__ __launch_bounds__(256) void k_enc_cmp_fused(const uint8_t *raw, uint8
         enc_xn_body<256, 0, IL>(raw, ahi, whi, blockIdx.x, lds);
     else
         compact_body<16, CWIN, 4, IL>(enc, alo, wlo, 1, has_off, blockIdx.x - nenc, lds);
+}
+
+// Encode and compaction in ONE launch (zr_rans_set_encode_fused, VERDICT r4
+// item 4): each 256-lane workgroup takes a ticket (its block, in buffer/block
+// order), encodes its 256 streams (k_enc_xn), publishes the block's byte sum with
+// the call's tag, and compacts its own 16 groups (k_enc_compact_lds) while its
+// scratch is recent (L2 / Infinity Cache), reading the sums of the buffer's lower
+// blocks by look-back. A workgroup waits only for lower tickets, taken by
+// workgroups already running or done, so nothing depends on residency or
+// dispatch order. The last workgroup to finish resets the call's ticket slot.
+// Short-stream (one window per group), <= 64-block, 256-lane batches only.
+__device__ unsigned int g_enc_tick[TT_SLOTS][2];
+__device__ __forceinline__ uint64_t lb_tag(uint64_t epoch) { return epoch % LB_TAGM + 1; }
+template <bool IL>
+__global__ __launch_bounds__(256) void k_enc_lb(const uint8_t *raw, uint8_t *enc, KArgs a, RansWork w, uint64_t epoch) {
+    constexpr uint32_t CWIN = 19 * 1024;
+    constexpr uint32_t LSZ = enc_xn_lds_bytes<256>() > sizeof(CmpLds<16, CWIN>) ? enc_xn_lds_bytes<256>()
+                                                                                 : (uint32_t)sizeof(CmpLds<16, CWIN>);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LSZ];
+    __shared__ uint32_t tkt;
+    unsigned int *const tk = g_enc_tick[epoch % TT_SLOTS];
+    if (threadIdx.x == 0) tkt = __hip_atomic_fetch_add(&tk[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t L = tkt;
+    const uint64_t tag = lb_tag(epoch);
+    enc_xn_body<256, 0, IL>(raw, a, w, L, lds, tag);
+    // this workgroup's scratch, lengths, offsets and states are read back by its
+    // own waves (same CU; no line of them was read before in this launch)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (uint32_t g = 0; g < 16; g++) {
+        compact_body<16, CWIN, 4, IL, 0, true>(enc, a, w, 1, 1, L * 16 + g, lds, tag);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(&tk[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x) {
+        __hip_atomic_store(&tk[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&tk[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // ======================================================================
@@ -3640,6 +3723,15 @@ const char *zr_rans_decoder_kernel(uint32_t n_buffers, uint32_t n_streams) {
     return dec_uses_dma(n_buffers, n_streams) ? "k_dec_xn_dma" : "k_dec_xn_fast";
 }
 
+int32_t zr_rans_set_encode_fused(int32_t on) {
+    clear_error();
+    if (on < 0 || on > 1) return set_error(ZR_INVALID_INPUT, "encode fused must be 0 or 1");
+    g_enc_fused.store(on, std::memory_order_relaxed);
+    return ZR_OK;
+}
+
+int32_t zr_rans_get_encode_fused(void) { return g_enc_fused.load(std::memory_order_relaxed); }
+
 int32_t zr_rans_set_encode_split(int32_t quarters) {
     clear_error();
     if (quarters < 0 || quarters > 3) return set_error(ZR_INVALID_INPUT, "encode split must be 0..3 quarters");
@@ -3840,7 +3932,18 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         const bool split = sq && !narrow && !wide && hB >= 1 && hB < a.B && (uint64_t)a.B * a.N >= (1u << 18) &&
                            w.nblk <= SCAN_FUSE && 256ull * w.cap < (1ull << 32) &&
                            (16ull * w.cap + 16) / (19 * 1024) / 2 <= 1 && kenc == (w.il ? k_enc_xn<256, 0, true> : k_enc_xn<256, 0, false>);
-        if (split) {
+        // fused (k_enc_lb): the 256-lane shape, short streams (one compaction
+        // window per group), the block sums scanned in the compaction, offsets from
+        // the encoder, a fresh call tag (not under capture)
+        constexpr uint32_t CWINF = 19 * 1024;
+        const bool fused = !split && !narrow && !wide && g_enc_fused.load(std::memory_order_relaxed) && w.il &&
+                           w.nblk <= SCAN_FUSE && 256ull * w.cap < (1ull << 32) &&
+                           (16ull * w.cap + 16) / CWINF / 2 <= 1 && !capturing(s) &&
+                           kenc == (w.il ? k_enc_xn<256, 0, true> : k_enc_xn<256, 0, false>);
+        if (fused) {
+            launch_timed("rans_encode", k_enc_lb<true>, dim3((uint32_t)gx), dim3(256), 0, s, raw, enc, a, w,
+                         next_epoch());
+        } else if (split) {
             const KArgs alo = kargs_sub(a, 0, hB), ahi = kargs_sub(a, hB, a.B - hB);
             const RansWork wlo = work_sub(w, a.N, 0), whi = work_sub(w, a.N, hB);
             const uint32_t nlo = hB * w.nblk, nhi = (a.B - hB) * w.nblk;  // encoder workgroups per half
@@ -3853,7 +3956,7 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         } else if (!narrow && !wide) {
             launch_timed("rans_encode", kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
         }
-        if (!split) {
+        if (!split && !fused) {
             if (w.nblk > SCAN_FUSE)  // (otherwise the compaction scans the block sums itself)
                 hipLaunchKernelGGL(k_scan, dim3(a.B), dim3(256), 0, s, a, w, 0);
             // 16 streams per group, 19 KiB windows (8 workgroups per CU), four 16-B loads in
