@@ -957,10 +957,15 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
         if (!DB) tile_sync();
         *reinterpret_cast<v4u *>(&tl[lr * EW + lp]) = pend;
         tile_sync();
-        if (body_ok && t >= 2) {  // (non-temporal: same-box A/B 0.244 -> 0.238 ms)
+        if (body_ok && t >= 2) {
+            // (default cache policy: round 2 measured non-temporal loads faster,
+            // 0.244 -> 0.238 ms encoder alone; round 5, same box, seven
+            // alternations of the whole step over two boxes: 0.5070 -> 0.5014 and
+            // 0.5012 -> 0.4941 ms with plain loads, the encoder the same, the
+            // decoder after it 4-6 us faster; profiles/r05_ab1.log, r05_ab2.log)
             gcu8 *rowb = uniform_ptr(inb + (uint64_t)(t - 1) * ETILE * N);
             typedef __attribute__((address_space(1))) const v4u gcv4u;
-            pend = __builtin_nontemporal_load((gcv4u *)(rowb + loff));
+            pend = *(gcv4u *)(rowb + loff);
         } else if (t > 0) {
             pend = issue_piece(t - 1);
         }
