@@ -184,6 +184,12 @@ int32_t zr_rans_set_decoder_ring(int32_t ring);
  * buffer, <= ~1.2 KiB of output per stream), not under graph capture. */
 int32_t zr_rans_set_encode_fused(int32_t on);
 int32_t zr_rans_get_encode_fused(void);
+/* Tuning (no reference counterpart): the stream compaction of an xN encode
+ * (batches of short streams, <= 64 blocks of 256 streams per buffer) as a
+ * software pipeline of wg_per_cu (1..8) workgroups per CU walking the 16-stream
+ * groups, 0 (the default) one workgroup per group; the same bytes
+ * (rans.rs:402-419). Measured slower. */
+int32_t zr_rans_set_compact_pipe(int32_t wg_per_cu);
 /* The name of the xN decode kernel a batch of n_buffers x n_streams (every
  * buffer at least n_streams bytes) runs under the current setting (reports and
  * profiles; a static string). */

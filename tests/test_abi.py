@@ -124,9 +124,19 @@ def test_diagnostic_switches_are_tools_only():
     import subprocess
     import sys
     src = open(os.path.join(ROOT, "zipora_amd", "csrc", "zr_rans.hip")).read()
+
+    def open_conditions(text):  # the preprocessor conditions open at the end of text
+        stack = []
+        for line in text.splitlines():
+            t = line.strip()
+            if t.startswith("#if"):
+                stack.append(t)
+            elif t.startswith("#endif"):
+                stack.pop()
+        return stack
+
     for m in re.finditer(r'getenv\("(ZR_[A-Z_]+)"\)', src):
-        head = src[:m.start()]
-        assert head.count("#ifdef ZR_DIAG") > head.count("#endif") - head.count("#ifndef"), m.group(1)
+        assert "#ifdef ZR_DIAG" in open_conditions(src[:m.start()]), m.group(1)
     env = dict(os.environ, ZR_ABLATE="1")
     r = subprocess.run([sys.executable, "-c", "import zipora_amd._lib as l; print(l.diag_env())"],
                        cwd=ROOT, env=env, capture_output=True, text=True)

@@ -95,6 +95,7 @@ SIGNATURES = [
     ("zr_rans_set_decoder_ring", ctypes.c_int32, [ctypes.c_int32]),
     ("zr_rans_set_encode_fused", ctypes.c_int32, [ctypes.c_int32]),
     ("zr_rans_get_encode_fused", ctypes.c_int32, []),
+    ("zr_rans_set_compact_pipe", ctypes.c_int32, [ctypes.c_int32]),
     ("zr_rans_decoder_kernel", ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint32]),
     ("zr_rans_get_encode_split", ctypes.c_int32, []),
     ("zr_rans_workspace_bytes", c_sz, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),

@@ -65,6 +65,16 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v, unsigned long long *sh
     return t;
 }
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
+    // the base is wave-uniform; say so, or the compiler may keep the descriptor
+    // in VGPRs and wrap every store in a readfirstlane loop
+    const uint64_t p = (uint64_t)base;
+    // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(u), 0, 0x7FFFFFFF, 0x00020000);
+}
+
 // sum over one wave (every lane gets it)
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 #pragma unroll
@@ -528,6 +538,9 @@ static std::atomic<int> g_enc_split{ZR_ENC_SPLIT_DEFAULT};
 #define ZR_ENC_FUSED_DEFAULT 0
 #endif
 static std::atomic<int> g_enc_fused{ZR_ENC_FUSED_DEFAULT};
+// the pipelined compaction (k_enc_compact_pipe): 0 off, else workgroups per CU
+// (zr_rans_set_compact_pipe); measured slower than k_enc_compact_lds, opt-in
+static std::atomic<int> g_cmp_pipe{0};
 #ifndef ZR_ENC_PF
 #define ZR_ENC_PF 1
 #endif
@@ -1219,7 +1232,10 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
     const uint32_t blk = grp / gpb, s0 = grp * CS;
     if (s0 >= N) return;
     const uint32_t ns = min(CS, N - s0);
-    const uint32_t tid = threadIdx.x;
+    // (tid opaque to the compiler: k_enc_compact_pipe runs this body inside its
+    // group loop, and values derived from tid hoisted out of it would stay live)
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63, wv = tid >> 6;
     uint8_t *dbase = enc + a.enc_off[b] + 12 * (size_t)N;
     // the chunks of stream i that land in the window [win, wend) of the image
@@ -1551,11 +1567,313 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
     }
 }
 
+#ifndef ZR_CMP_GRID
+#define ZR_CMP_GRID 0  // > 0: the compaction as a grid-stride loop over 256 * ZR_CMP_GRID workgroups
+#endif
 template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_lds(
     uint8_t *enc, KArgs a, RansWork w, uint32_t nwin, int has_off) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[sizeof(CmpLds<CS, CWIN>)];
+#if ZR_CMP_GRID
+    // grid-stride over the groups' windows (fewer, longer-lived workgroups)
+    const uint32_t nv = a.B * w.nblk * (256 / CS) * nwin;
+    for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
+        compact_body<CS, CWIN, CU_LD, IL, ABL>(enc, a, w, nwin, has_off, v, smem);
+        __syncthreads();
+    }
+#else
     compact_body<CS, CWIN, CU_LD, IL, ABL>(enc, a, w, nwin, has_off, blockIdx.x, smem);
+#endif
+}
+
+// The compaction as a software pipeline (the headline path: lane-interleaved
+// scratch, stream offsets left by the 256-lane encoder, <= SCAN_FUSE blocks per
+// buffer). k_enc_compact_lds gives every group its own workgroup, whose three
+// steps run one after the other: the setup loads, the scratch loads, the
+// stores. Its ablations (profiles/r05_cmp_abl.log) put that skeleton alone at
+// 0.0375 of 0.114 ms, and the loads alone at 4.2 TB/s: most of a workgroup's
+// life has nothing in flight. Here a workgroup walks the groups gid =
+// blockIdx.x + k * gridDim.x with three of them under way at once: while group
+// k's image is stored, group k+1's scratch loads are in flight and wave 0 sets
+// group k+2 up from the loads it issued one group earlier (two setup slots in
+// LDS). A group whose image is wider than the window, or whose longest stream
+// has more chunk rows than a lane's loads cover, runs k_enc_compact_lds's body
+// in place (same bytes, its own loads).
+constexpr uint32_t CP_NV = 5;                // 16-B chunk loads per lane per group
+constexpr uint32_t CP_ROWS = 4 * 64 * CP_NV / 16;  // chunk rows of a group the loads cover (80)
+struct CpSlot {
+    int4 ilm[16];    // per stream: chunk rows [0, y), image bytes [z, w)
+    uint64_t uoff;   // image byte 0 at enc + uoff (16-B aligned)
+    uint32_t kind;   // 0 nothing to store, 1 pipelined, 2 the in-place body
+    uint32_t rows, span, lo;  // chunk rows; image bytes; the group's first byte in the image
+};
+// the workgroup's groups that take the in-place body, one bit per loop step
+// (run after the loop, when none of the pipeline's registers is live)
+constexpr uint32_t CP_MAXK = 512;  // loop steps per workgroup (the host checks)
+// wave 0's setup loads of the next group, landed in LDS by DMA (no registers
+// held through the step): the buffer's block sums (lanes < nblk), the group's
+// lengths, in-block offsets and final states (lanes < 16), the buffer's length
+// and encoded offset (lanes 0, 1)
+struct CpMeta {
+    uint32_t bslo[64], bshi[64], L[16], o[16], X[16], len[2], eoff[2];
+};
+constexpr uint32_t CP_WIN = 19 * 1024 - 2 * (uint32_t)sizeof(CpSlot) - CP_MAXK / 8 - (uint32_t)sizeof(CpMeta);
+constexpr uint32_t CP_LDS = (uint32_t)sizeof(CmpLds<16, CP_WIN>) + 2 * (uint32_t)sizeof(CpSlot) + CP_MAXK / 8 +
+                            (uint32_t)sizeof(CpMeta);
+// one 4-byte LDS DMA per lane: lane l's dword at g lands at LDS address dst + 4 l.
+// (asm: the compiler neither counts it, so it adds no wait for it, nor sees its
+// LDS write, so it adds no wait before later LDS reads; M0 is restored; the nop
+// is the wait state between the M0 write and the DMA reading it)
+__device__ __forceinline__ void cp_dma4(const void *g, uint32_t dst) {
+    uint32_t save;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(save)
+                 : "v"(g), "s"(dst)
+                 : "memory");
+}
+constexpr uint32_t CP_NS = (CP_WIN / 16 + 255) / 256;  // 16-B unit stores per lane per group
+static_assert(CP_WIN % 16 == 0, "16-B image units");
+static_assert(CP_LDS <= 160 * 1024 / 8, "8 workgroups per CU");
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_pipe(
+    uint8_t *enc, KArgs a, RansWork w) {
+    constexpr uint32_t CS = 16;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[CP_LDS];
+    CpSlot *const slot = reinterpret_cast<CpSlot *>(smem + sizeof(CmpLds<CS, CP_WIN>));
+    uint32_t *const slowm = reinterpret_cast<uint32_t *>(smem + sizeof(CmpLds<CS, CP_WIN>) + 2 * sizeof(CpSlot));
+    constexpr uint32_t MOFF = (uint32_t)sizeof(CmpLds<CS, CP_WIN>) + 2 * (uint32_t)sizeof(CpSlot) + CP_MAXK / 8;
+    const CpMeta &M = *reinterpret_cast<const CpMeta *>(smem + MOFF);
+    const uint32_t mlds = (uint32_t)(uintptr_t)(smem + MOFF);  // (LDS address)
+    uint8_t *const img = reinterpret_cast<CmpLds<CS, CP_WIN> *>(smem)->img;
+    const uint32_t tid = threadIdx.x, wv = tid >> 6;
+    // lane: re-made opaque to the compiler every loop step, so that no value
+    // derived from it is hoisted out of the loop and kept live through it (64
+    // VGPRs at 8 waves per SIMD)
+    uint32_t lane = tid & 63;
+    const uint32_t N = a.N, nblk = w.nblk, ngrp = nblk * (256 / CS), ng = a.B * ngrp;
+    const uint32_t G = gridDim.x;
+    // wave 0: issue the setup loads of one group (one memory round trip, into M)
+    auto meta_load = [&](uint32_t gid) __attribute__((always_inline)) {
+        if (gid >= ng) return;
+        const uint32_t b = __builtin_amdgcn_readfirstlane(gid / ngrp);
+        const uint32_t s0 = __builtin_amdgcn_readfirstlane((gid % ngrp) * CS);
+        if (s0 >= N) return;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // setup's reads of M are done
+        if (lane < nblk) {
+            const uint32_t *bs = reinterpret_cast<const uint32_t *>(w.blocksum + (size_t)b * nblk + lane);
+            cp_dma4(bs, mlds + offsetof(CpMeta, bslo));
+            cp_dma4(bs + 1, mlds + offsetof(CpMeta, bshi));
+        }
+        if (lane < min(CS, N - s0)) {
+            const size_t k = (size_t)b * N + s0 + lane;
+            cp_dma4(w.st_len + k, mlds + offsetof(CpMeta, L));
+            cp_dma4(w.st_off + k, mlds + offsetof(CpMeta, o));
+            cp_dma4(w.st_state + k, mlds + offsetof(CpMeta, X));
+        }
+        if (lane < 2) {
+            cp_dma4(reinterpret_cast<const uint32_t *>(a.len + b) + lane, mlds + offsetof(CpMeta, len));
+            cp_dma4(reinterpret_cast<const uint32_t *>(a.enc_off + b) + lane, mlds + offsetof(CpMeta, eoff));
+        }
+    };
+    // wave 0: the group's offsets, header words, status (its buffer's group 0)
+    // and image layout, into a slot
+    auto setup = [&](uint32_t gid, CpSlot &S) __attribute__((always_inline)) {
+        uint32_t kind = 0;
+        if (gid < ng) {
+            const uint32_t b = __builtin_amdgcn_readfirstlane(gid / ngrp);
+            const uint32_t grp = __builtin_amdgcn_readfirstlane(gid % ngrp), blk = grp / (256 / CS), s0 = grp * CS;
+            const uint64_t mn = (uint64_t)M.len[0] | ((uint64_t)M.len[1] << 32);
+            if (s0 < N && !single_mode(mn, N)) {
+                const uint32_t ns = min(CS, N - s0);
+                const uint64_t mbs = lane < nblk ? (uint64_t)M.bslo[lane] | ((uint64_t)M.bshi[lane] << 32) : 0;
+                const uint32_t mL = lane < ns ? M.L[lane] : 0u, mo = lane < ns ? M.o[lane] : 0u;
+                const uint32_t mX = lane < ns ? M.X[lane] : 0u;
+                const uint64_t meo = (uint64_t)M.eoff[0] | ((uint64_t)M.eoff[1] << 32);
+                const uint64_t c = mbs & ~BS_ERR;
+                const uint64_t below = wave_sum(lane < blk ? c : 0);
+                const bool flagged = __any((mbs >> 63) != 0);
+                if (grp == 0) {
+                    const uint64_t tot = wave_sum(c);
+                    if (lane == 0) {
+                        a.enc_len[b] = (uint64_t)N * 12 + tot;
+                        a.status[b] = flagged ? ZR_INVALID_INPUT : ZR_OK;  // the only status writer of an xN encode
+                    }
+                }
+                if (!flagged) {
+                    const bool mine = lane < ns;
+                    const uint64_t eoff = meo;
+                    uint8_t *const e = enc + eoff;
+                    const uint64_t off = (uint64_t)mo + below;  // the stream's offset in the buffer's streams
+                    if (mine) {
+                        const uint32_t sb = s0 + lane;
+                        if ((((uintptr_t)e) & 7) == 0) {
+                            *reinterpret_cast<uint2 *>(e + 8 * (size_t)sb) = make_uint2(mX, 0);
+                            *reinterpret_cast<uint32_t *>(e + 8 * (size_t)N + 4 * (size_t)sb) = mL;
+                        } else {
+                            st_u32_u(e + 8 * (size_t)sb, mX);
+                            st_u32_u(e + 8 * (size_t)sb + 4, 0);
+                            st_u32_u(e + 8 * (size_t)N + 4 * (size_t)sb, mL);
+                        }
+                    }
+                    const uint64_t r0 = __shfl(off, 0, 64), r1 = __shfl(off + mL, (int)ns - 1, 64);
+                    if (r1 > r0) {
+                        const uint64_t d0 = eoff + 12 * (uint64_t)N;  // the streams' first byte, from enc
+                        const uint64_t u0 = (((uintptr_t)enc + d0 + r0) & ~(uintptr_t)15) - (uintptr_t)enc;
+                        const uint64_t span = d0 + r1 - u0;
+                        uint32_t rows = mine ? (mL + 15) >> 4 : 0;
+#pragma unroll
+                        for (int d = 1; d < 16; d <<= 1) rows = max(rows, (uint32_t)__shfl_xor((int)rows, d, 64));
+                        kind = span <= CP_WIN && rows <= CP_ROWS ? 1 : 2;
+                        if (lane < 16) {
+                            const int32_t D = (int32_t)(d0 + off - u0);
+                            S.ilm[lane] = mine && mL ? make_int4(0, (int32_t)((mL + 15) >> 4), D, D + (int32_t)mL)
+                                                     : make_int4(0, 0, 0, 0);
+                        }
+                        if (lane == 0) {
+                            S.uoff = u0;
+                            S.rows = rows;
+                            S.span = (uint32_t)min<uint64_t>(span, 0xFFFFFFFFu);
+                            S.lo = (uint32_t)(d0 + r0 - u0);
+                        }
+                    }
+                }
+            }
+        }
+        if (lane == 0) S.kind = kind;
+    };
+    // the group's scratch column of this lane's stream (lane % 16)
+    auto scol_of = [&](uint32_t gid) __attribute__((always_inline)) {
+        const uint32_t b = __builtin_amdgcn_readfirstlane(gid / ngrp);
+        const uint32_t s0 = __builtin_amdgcn_readfirstlane((gid % ngrp) * CS);
+        return w.scratch + (size_t)b * w.region + (size_t)(s0 & ~63u) * w.cap + ((s0 & 63u) + lane % CS) * 16;
+    };
+    v4u v[CP_NV];
+    // all lanes: the group's chunks, quad row c of stream lane % 16 (rows past the
+    // stream's last read its row 0 again: one cached line, no branch)
+    auto prefetch = [&](uint32_t gid, const CpSlot &S) __attribute__((always_inline)) {
+        // (t: tid the compiler cannot see through, so that the chunk coordinates are
+        // not hoisted out of the group loop into registers; 64 VGPRs at 8 waves per SIMD)
+        uint32_t t = tid;
+        asm volatile("" : "+v"(t));
+        const bool on = gid < ng && S.kind == 1;
+        const uint8_t *const col = on ? scol_of(gid) : w.scratch;
+        const uint32_t y = on ? (uint32_t)S.ilm[t % CS].y : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < CP_NV; k++) {
+            const uint32_t c = ((t >> 6) * 64 * CP_NV + 64 * k + (t & 63)) / CS;
+            v[k] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(col + (c < y ? c * 1024 : 0u)));
+        }
+    };
+    // all lanes: the chunks into the image at their destination offsets
+    auto land = [&](const CpSlot &S) __attribute__((always_inline)) {
+        uint32_t t = tid;
+        asm volatile("" : "+v"(t));
+        const int4 mi = S.ilm[t % CS];
+        const int32_t wl = (int32_t)S.span;
+#pragma unroll
+        for (uint32_t k = 0; k < CP_NV; k++) {
+            const uint32_t c = ((t >> 6) * 64 * CP_NV + 64 * k + (t & 63)) / CS;
+            if ((int32_t)c >= mi.y) continue;
+            const int32_t p = mi.z + 16 * (int32_t)c;
+            const int32_t nvk = min(16, mi.w - p);
+            if (nvk == 16 && p >= 0 && p + 16 <= wl) {
+                // (as k_enc_compact_lds: the chunk shifted to the dword grid)
+                const uint32_t x0 = v[k].x, x1 = v[k].y, x2 = v[k].z, x3 = v[k].w;
+                const uint32_t al = (uint32_t)p & 3, sh = 32 - 8 * al;
+                const int32_t q = p - (int32_t)al;
+                const uint32_t d0 = (uint32_t)(((uint64_t)x0 << 32) >> sh);
+                const uint32_t d4 = (uint32_t)((uint64_t)x3 >> sh);
+                uint32_t *m = reinterpret_cast<uint32_t *>(img + q + 4);
+                m[0] = (uint32_t)((((uint64_t)x1 << 32) | x0) >> sh);
+                m[1] = (uint32_t)((((uint64_t)x2 << 32) | x1) >> sh);
+                m[2] = (uint32_t)((((uint64_t)x3 << 32) | x2) >> sh);
+                if (al == 0) *reinterpret_cast<uint32_t *>(img + q) = d0;
+                if (al & 1) img[q + al] = (uint8_t)(d0 >> (8 * al));
+                if (al == 1 || al == 2) *reinterpret_cast<uint16_t *>(img + q + 2) = (uint16_t)(d0 >> 16);
+                if (al >= 2) *reinterpret_cast<uint16_t *>(img + q + 16) = (uint16_t)d4;
+                if (al & 1) img[q + 16 + (al & 2)] = (uint8_t)(d4 >> (8 * (al & 2)));
+            } else {  // a stream's last chunk
+                const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                for (int32_t j = 0; j < nvk; j++) {
+                    const int32_t q = p + j;
+                    if (q >= 0 && q < wl) img[q] = (uint8_t)(wd[j >> 2] >> (8 * (j & 3)));
+                }
+            }
+        }
+    };
+    // prologue: groups 0 and 1 set up, group 2's loads issued, group 0's chunks in flight
+    const uint32_t g0 = blockIdx.x;
+    if (tid < CP_MAXK / 32) slowm[tid] = 0;
+    if (wv == 0) {
+        meta_load(g0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        setup(g0, slot[0]);
+        meta_load(g0 + G);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        setup(g0 + G, slot[1]);
+        meta_load(g0 + 2 * G);
+    }
+    __syncthreads();
+    prefetch(g0, slot[0]);
+    for (uint32_t j = 0; j < CP_NS; j++)  // (dropped: the count the loop's stores keep; distinct, not merged)
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{0, 0, 0, 0}, byte_rsrc(enc), 0x80000000u + 16 * j, 0, 2);
+    for (uint32_t k = 0, gid = g0; gid < ng; k++, gid += G) {
+        lane = tid & 63;
+        asm volatile("" : "+v"(lane));
+        CpSlot &S = slot[k & 1];
+        const uint32_t kind = S.kind;
+        // (the compiler's wait for the chunk loads: CP_NS unit stores were issued
+        // after them in every wave, the prologue's included, and wave 0's setup
+        // DMAs before those, uncounted: vmcnt(CP_NS), the stores stay in flight)
+        if (kind == 1) land(S);
+        const bool st = kind == 1;
+        const uint64_t uoff = st ? S.uoff : 0;
+        const uint32_t span = st ? S.span : 0, lo = st ? S.lo : 0;
+        __syncthreads();  // the image is whole; slot k & 1 is free
+        if (kind == 2 && tid == 0) slowm[k / 32] |= 1u << (k % 32);
+        if (wv == 0) {
+            // M holds group k + 2's setup loads: its DMAs were issued before the
+            // last CP_NS stores of the step before (land's waits may have been
+            // skipped with its chunks)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(CP_NS) : "memory");
+            setup(gid + 2 * G, S);
+            // the group's two edge units (shared with the neighbouring groups), byte
+            // by byte, lanes 0 and 1; before the chunk loads, so that every wave
+            // issues the same number of stores after them
+            const uint32_t nunit = (span + 15) / 16;
+            const uint32_t u = lane == 0 ? 0 : nunit - 1;
+            if (lane < 2 && nunit && (lane == 0 || nunit > 1) && !(16 * u >= lo && 16 * u + 16 <= span)) {
+                uint8_t *const dst = enc + uoff + 16 * (uint64_t)u;
+                for (uint32_t j = 0; j < 16; j++) {
+                    const uint32_t q = 16 * u + j;
+                    if (q >= lo && q < span) dst[j] = img[q];
+                }
+            }
+        }
+        prefetch(gid + G, slot[(k + 1) & 1]);
+        if (wv == 0) meta_load(gid + 3 * G);
+        // the image out in whole 16-B units (out-of-range offsets drop the rest):
+        // the last CP_NS vector memory operations of every wave
+        {
+            const __amdgpu_buffer_rsrc_t r = byte_rsrc(enc + uoff);
+            const uint32_t nunit = (span + 15) / 16;
+#pragma unroll
+            for (uint32_t j = 0; j < CP_NS; j++) {
+                const uint32_t u = wv * 64 + lane + 256 * j;
+                const bool full = u < nunit && 16 * u >= lo && 16 * u + 16 <= span;
+                const v4u x = *reinterpret_cast<const v4u *>(img + 16 * (u < CP_WIN / 16 ? u : 0));
+                __builtin_amdgcn_raw_buffer_store_b128(x, r, full ? 16 * u : 0x80000000u, 0, 2);
+            }
+        }
+        __syncthreads();  // the image is free; slot k & 1 holds group k + 2
+    }
+    // the groups wider than the window
+    for (uint32_t k = 0, gid = g0; gid < ng; k++, gid += G) {
+        if (slowm[k / 32] & (1u << (k % 32))) {
+            compact_body<CS, CP_WIN, 4, true>(enc, a, w, 1, 1, gid, smem);
+            __syncthreads();
+        }
+    }
 }
 
 // The second launch of a split encode (zr_rans_encode_batch_dev, SPLIT): the
@@ -1703,15 +2021,6 @@ __device__ __noinline__ bool dec_lane_generic(const RansDTab *T, const uint32_t 
 }
 constexpr int DT2 = 16;  // steps per tile
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
-    // the base is wave-uniform; say so, or the compiler may keep the descriptor
-    // in VGPRs and wrap every store in a readfirstlane loop
-    const uint64_t p = (uint64_t)base;
-    // (readfirstlane returns int: widen through uint32_t, never sign-extend)
-    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p) |
-                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(u), 0, 0x7FFFFFFF, 0x00020000);
-}
 
 // FW: workgroup width (1024 = one workgroup per CU sharing one table copy at
 // 2^18 streams; 64 = one wave per workgroup, which spreads a batch of few
@@ -3738,6 +4047,13 @@ int32_t zr_rans_set_encode_fused(int32_t on) {
 
 int32_t zr_rans_get_encode_fused(void) { return g_enc_fused.load(std::memory_order_relaxed); }
 
+int32_t zr_rans_set_compact_pipe(int32_t wg_per_cu) {
+    clear_error();
+    if (wg_per_cu < 0 || wg_per_cu > 8) return set_error(ZR_INVALID_INPUT, "compact pipe must be 0..8");
+    g_cmp_pipe.store(wg_per_cu, std::memory_order_relaxed);
+    return ZR_OK;
+}
+
 int32_t zr_rans_set_encode_split(int32_t quarters) {
     clear_error();
     if (quarters < 0 || quarters > 3) return set_error(ZR_INVALID_INPUT, "encode split must be 0..3 quarters");
@@ -3992,8 +4308,19 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             // the 256-lane encoder leaves each stream's offset in its block (a
             // block's bytes fit 32 bits: 256 * cap < 2^32)
             const int has_off = !narrow && 256ull * w.cap < (1ull << 32);
-            launch_timed("rans_compact", kcmp, dim3((uint32_t)(gx * 16 * nwin)), dim3(256), 0, s, enc, a, w, nwin,
-                         has_off);
+#if ZR_CMP_GRID
+            const uint32_t gcmp = (uint32_t)std::min<uint64_t>(gx * 16 * nwin, 256u * ZR_CMP_GRID);
+#else
+            const uint32_t gcmp = (uint32_t)(gx * 16 * nwin);
+#endif
+            const uint32_t wpc = (uint32_t)g_cmp_pipe.load(std::memory_order_relaxed);
+            const uint32_t gp = (uint32_t)std::min<uint64_t>(gx * 16, (uint64_t)cu_count() * wpc);
+            if (wpc && w.il && has_off && w.nblk <= SCAN_FUSE && gp && (gx * 16 + gp - 1) / gp <= CP_MAXK) {
+                // the pipelined compaction: wpc workgroups per CU walk the groups
+                launch_timed("rans_compact", k_enc_compact_pipe, dim3(gp), dim3(256), 0, s, enc, a, w);
+            } else {
+                launch_timed("rans_compact", kcmp, dim3(gcmp), dim3(256), 0, s, enc, a, w, nwin, has_off);
+            }
         }
     }
     timer_begin("rans_encode_x1", s);
