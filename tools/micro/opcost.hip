@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #define ITERS 2048
 
@@ -56,6 +57,17 @@ __global__ __launch_bounds__(1024) void k(uint32_t *out, uint64_t *cyc, uint32_t
             if (OP == 22) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));
             if (OP == 23) asm volatile("v_lshlrev_b32 %0, %1, %0" : "+v"(a[c]) : "v"(b));
             if (OP == 24) asm volatile("v_or3_b32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if (OP == 25) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));
+            if (OP == 26) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));
+            if (OP == 27) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a[c]) : "v"(b));
+            if (OP == 28) asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(a[c]));
+            if (OP == 29) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(a[c]) : "v"(b));
+            if (OP == 30) asm volatile("v_cmp_lt_u32_e64 s[40:41], %0, %1\n\tv_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(a[c]) : "v"(b) : "s40", "s41");
+            if (OP == 31) asm volatile("v_cmp_lt_u32_e32 vcc, %0, %1\n\tv_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[c]) : "v"(b) : "vcc");
+            if (OP == 32) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));
+            if (OP == 33) asm volatile("v_med3_u32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if (OP == 34) asm volatile("v_lshrrev_b32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "+v"(a[c]) : "v"(b));
+            if (OP == 35) asm volatile("v_sub_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %0, vcc, %0, 0, vcc" : "+v"(a[c]) : "v"(b) : "vcc");
         }
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -98,6 +110,23 @@ int main() {
     uint64_t *cyc;
     hipMalloc(&out, 1 << 26);
     hipMalloc(&cyc, 1 << 16);
+    for (int w : {4}) {
+        run<25>("v_mul_hi_u32", out, cyc, w);
+        run<26>("v_mul_lo_u32", out, cyc, w);
+        run<27>("v_mul_f32", out, cyc, w);
+        run<28>("v_cvt_f32_u32", out, cyc, w);
+        run<29>("v_mul_hi_u32_u24", out, cyc, w);
+        run<30>("cmp_e64+cndmask (2)", out, cyc, w);
+        run<31>("cmp_e32+cndmask (2)", out, cyc, w);
+        run<32>("v_max_u32", out, cyc, w);
+        run<33>("v_med3_u32", out, cyc, w);
+        run<34>("lshrrev_sdwa", out, cyc, w);
+        run<35>("sub_co+addc (2)", out, cyc, w);
+        run<7>("v_mad_u32_u24", out, cyc, w);
+        run<6>("v_bfe_u32", out, cyc, w);
+        run<0>("v_add_u32", out, cyc, w);
+    }
+    if (getenv("OPCOST_ALL") == nullptr) return 0;
     for (int w : {8}) {
         run<16>("v_and literal", out, cyc, w);
         run<17>("v_and sgpr", out, cyc, w);

@@ -104,10 +104,11 @@ struct RansWork {
     uint64_t region;      // R: scratch bytes per buffer
     uint32_t cap;         // scratch bytes per stream (xN mode), a multiple of 16
     uint32_t nblk;
-    // xN scratch layout. il = 1 (short streams): the 64 streams of a wave group
-    // s & ~63 share 64 * cap bytes, 16-B quad q of stream s at ((q * 64 + (s & 63)) * 16)
-    // (the encoder's burst stores coalesce across lanes). il = 0: stream s owns
-    // cap contiguous bytes at s * cap
+    // xN scratch layout. il = 1 (short streams): the IL_SPAN (zr_rans.hip, 64)
+    // streams of a group s & ~(IL_SPAN - 1) share IL_SPAN * cap bytes, 16-B quad q
+    // of stream s at ((q * IL_SPAN + s % IL_SPAN) * 16) (the encoder's burst stores
+    // coalesce across lanes into 1 KiB runs). il = 0: stream s owns cap contiguous
+    // bytes at s * cap
     uint32_t il;
 };
 size_t rans_workspace_bytes(uint32_t B, uint32_t N, uint64_t max_len);

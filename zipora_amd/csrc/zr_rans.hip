@@ -22,6 +22,17 @@ namespace zr {
 // ------------------------------------------------------------------ helpers
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
+// the lane-interleaved xN scratch (RansWork::il): the IL_SPAN streams of a group
+// interleaved quad by quad, quad q of stream s at ((q * IL_SPAN + s % IL_SPAN) * 16)
+// in the group's IL_SPAN * cap bytes. 64 (a wave's streams: its burst stores are
+// 1 KiB runs); 16 (one compaction group, whose chunk rows are then one run) was
+// measured slower: encoder 0.166 -> 0.175 ms, compaction unchanged
+// (profiles/r05_ab9.log)
+#ifndef ZR_IL_SPAN
+#define ZR_IL_SPAN 64
+#endif
+constexpr uint32_t IL_SPAN = ZR_IL_SPAN;
+static_assert(IL_SPAN == 16 || IL_SPAN == 64, "a compaction group (16 streams) lies in one interleave span");
 __device__ __forceinline__ uint32_t ld_u32_u(const uint8_t *p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
@@ -727,10 +738,11 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
         }
         return v;
     };
-    // scratch: quad q (16 B) of this stream at qbase + q * qstride (RansWork::il)
-    const uint32_t ln = tid & 63;  // = s & 63
+    // scratch: quad q (16 B) of this stream at qbase + q * qstride (RansWork::il:
+    // the IL_SPAN streams of a group interleaved quad by quad)
+    const uint32_t ln = tid & (IL_SPAN - 1);  // = s % IL_SPAN
     uint8_t *const qbase = w.scratch + (size_t)b * w.region + (size_t)(s - ln) * w.cap + (IL ? ln * 16 : (size_t)ln * w.cap);
-    constexpr uint32_t qstride = IL ? 64 * 16 : 16;
+    constexpr uint32_t qstride = IL ? IL_SPAN * 16 : 16;
     auto quad = [&](uint32_t q) -> v4u * { return reinterpret_cast<v4u *>(qbase + q * qstride); };
     auto dword = [&](uint32_t d) -> uint32_t * {
         return reinterpret_cast<uint32_t *>(qbase + (d >> 2) * qstride + (d & 3) * 4);
@@ -1422,9 +1434,9 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
     if (r1 <= r0) return;
     ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
     span = (uintptr_t)dbase + r1 - ua0;  // bytes of the image from ua0
-    // stream-major: stream i's chunk c at sbase + i * cap + 16 c; IL: at sbase + (64 c + i) * 16
+    // stream-major: stream i's chunk c at sbase + i * cap + 16 c; IL: at sbase + (IL_SPAN c + i) * 16
     const uint8_t *sbase = w.scratch + (size_t)b * w.region +
-                           (IL ? (size_t)(s0 & ~63u) * w.cap + (s0 & 63u) * 16 : (size_t)s0 * w.cap);
+                           (IL ? (size_t)(s0 & ~(IL_SPAN - 1)) * w.cap + (s0 & (IL_SPAN - 1)) * 16 : (size_t)s0 * w.cap);
     const uint64_t lo = (uintptr_t)dbase + r0 - ua0;  // image bytes below lo belong to another group
     for (uint64_t win = (uint64_t)wi * CWIN; win < span; win += (uint64_t)nwin * CWIN) {
         const uint64_t wend = min(span, win + (uint64_t)CWIN);
@@ -1470,7 +1482,7 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
                 if (IL) {
                     const uint32_t c = qrow0 + f / CS;
                     if (f < nchunks && (int32_t)c >= mi.x && (int32_t)c < mi.y) {
-                        src = scol + c * 1024;
+                        src = scol + c * (IL_SPAN * 16);
                         dpos[k] = mi.z + 16 * (int32_t)c;
                         nv[k] = (uint32_t)min(16, mi.w - dpos[k]);
                     }
@@ -1745,7 +1757,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     auto scol_of = [&](uint32_t gid) __attribute__((always_inline)) {
         const uint32_t b = __builtin_amdgcn_readfirstlane(gid / ngrp);
         const uint32_t s0 = __builtin_amdgcn_readfirstlane((gid % ngrp) * CS);
-        return w.scratch + (size_t)b * w.region + (size_t)(s0 & ~63u) * w.cap + ((s0 & 63u) + lane % CS) * 16;
+        return w.scratch + (size_t)b * w.region + (size_t)(s0 & ~(IL_SPAN - 1)) * w.cap +
+               ((s0 & (IL_SPAN - 1)) + lane % CS) * 16;
     };
     v4u v[CP_NV];
     // all lanes: the group's chunks, quad row c of stream lane % 16 (rows past the
@@ -1761,7 +1774,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 #pragma unroll
         for (uint32_t k = 0; k < CP_NV; k++) {
             const uint32_t c = ((t >> 6) * 64 * CP_NV + 64 * k + (t & 63)) / CS;
-            v[k] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(col + (c < y ? c * 1024 : 0u)));
+            v[k] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(col + (c < y ? c * (IL_SPAN * 16) : 0u)));
         }
     };
     // all lanes: the chunks into the image at their destination offsets
