@@ -53,7 +53,8 @@ def main():
     traffic = {}
     for tag, fsub, wsub in (("rans", "pmc_fetch", "pmc_write"), ("rans_literal", "pmc_lit_fetch", "pmc_lit_write"),
                             ("fse64", "pmc_fse_fetch", "pmc_fse_write"), ("blob", "pmc_blob_fetch", "pmc_blob_write"),
-                            ("o1", "pmc_o1_fetch", "pmc_o1_write")):
+                            ("o1", "pmc_o1_fetch", "pmc_o1_write"),
+                            ("rans_n2e18", "pmc_n18_fetch", "pmc_n18_write")):
         fc, wc = counters(d, fsub), counters(d, wsub)
         ks = sorted({k for k, _ in fc} | {k for k, _ in wc})
         if ks:
