@@ -1204,6 +1204,22 @@ __global__ __launch_bounds__(64) void k_enc_x1_compact(uint8_t *enc, KArgs a, Ra
 // LDS image writes, 4 phase-1 loads all read the group's first 256 B
 // the compaction's LDS (one struct, so that k_enc_cmp_fused can lay it over
 // the encoder's)
+// bytes [a, b) of a 16-B unit (a, b <= 16) from the LDS image to a 16-B aligned
+// destination, in naturally aligned pieces: at most 7 stores (up to 16 byte stores
+// before; a group's two edge units were as many store instructions as its body)
+__device__ __forceinline__ void unit_range_store(uint8_t *dst, const uint8_t *src, uint32_t a, uint32_t b) {
+    if (a >= b) return;
+    if ((a & 1) && a + 1 <= b) { dst[a] = src[a]; a += 1; }
+    if ((a & 2) && a + 2 <= b) { *reinterpret_cast<uint16_t *>(dst + a) = *reinterpret_cast<const uint16_t *>(src + a); a += 2; }
+    if ((a & 4) && a + 4 <= b) { *reinterpret_cast<uint32_t *>(dst + a) = *reinterpret_cast<const uint32_t *>(src + a); a += 4; }
+    if ((a & 8) && a + 8 <= b) { *reinterpret_cast<uint64_t *>(dst + a) = *reinterpret_cast<const uint64_t *>(src + a); a += 8; }
+    // (a + s <= b below implies every head step above had room: a is s-aligned)
+    if (a + 8 <= b) { *reinterpret_cast<uint64_t *>(dst + a) = *reinterpret_cast<const uint64_t *>(src + a); a += 8; }
+    if (a + 4 <= b) { *reinterpret_cast<uint32_t *>(dst + a) = *reinterpret_cast<const uint32_t *>(src + a); a += 4; }
+    if (a + 2 <= b) { *reinterpret_cast<uint16_t *>(dst + a) = *reinterpret_cast<const uint16_t *>(src + a); a += 2; }
+    if (a < b) dst[a] = src[a];
+}
+
 template <uint32_t CS, uint32_t CWIN>
 struct CmpLds {
     unsigned long long sh[4];
@@ -1218,7 +1234,9 @@ struct CmpLds {
 // them for the status writer, group 0 of the buffer's LAST block, whose blocks
 // all took lower tickets). Flags are checked over the same blocks.
 constexpr uint64_t LB_SUM = (1ull << 40) - 1, LB_TAGM = (1ull << 23) - 1;
-template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0, bool LB = false>  // streams per group (divides 64), window bytes, loads in flight
+// NT: threads per workgroup (256; 128 only with the encoder's stream offsets and
+// <= SCAN_FUSE blocks per buffer: the block-scan path needs four waves)
+template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0, bool LB = false, uint32_t NT = 256>  // streams per group (divides 64), window bytes, loads in flight
 __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const RansWork &w, uint32_t nwin,
                                              int has_off, uint32_t vblk, uint8_t *const smem, uint64_t lbtag = 0) {
     static_assert(CS <= 64 && 64 % CS == 0, "a group's streams are lanes of one wave");
@@ -1376,6 +1394,8 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
         }
         __syncthreads();
         if (sfail) return;
+    } else if constexpr (NT != 256) {
+        return;  // (not launched: the host takes k_enc_compact_lds<.., 256> there)
     } else {
     // the buffer's scan of block byte sums (k_scan, fused): this block's
     // offset, and for group 0 the encoded length and the final status
@@ -1470,7 +1490,7 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
         const int4 mi = IL ? ilm[lane % CS] : make_int4(0, 0, 0, 0);
         const uint8_t *scol = sbase + (lane % CS) * 16;
         uint32_t si = 0;
-        for (uint32_t f0 = wv * 64 * CU_LD; f0 < nchunks; f0 += 256 * CU_LD) {
+        for (uint32_t f0 = wv * 64 * CU_LD; f0 < nchunks; f0 += NT * CU_LD) {
             v4u v[CU_LD];
             int32_t dpos[CU_LD];  // image position of the chunk's first byte (relative to win)
             uint32_t nv[CU_LD];   // valid bytes of the chunk
@@ -1557,7 +1577,7 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
         __syncthreads();
         // ---- phase 2: LDS image -> destination, aligned 16-B units
         const uint32_t nunit = (wl + 15) / 16;
-        for (uint32_t u = tid; u < nunit; u += 256) {
+        for (uint32_t u = tid; u < nunit; u += NT) {
             const uint64_t q0 = win + 16 * (uint64_t)u;  // image offset of the unit
             // (pointer arithmetic from dbase, not an integer cast: a flat store
             // counts in lgkmcnt, so the LDS waits and barriers after it would
@@ -1570,31 +1590,35 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
                 // (same-box A/B: the decode that reads them 0.200 -> 0.180 ms, the
                 // compaction itself unchanged)
                 __builtin_nontemporal_store(*reinterpret_cast<const v4u *>(img + 16 * u), reinterpret_cast<v4u *>(dst));
-            } else {
-                for (uint32_t t = 0; t < 16; t++)
-                    if (q0 + t >= lo && q0 + t < span) dst[t] = img[16 * u + t];
+            } else if (q0 + 16 > lo && q0 < span) {
+                unit_range_store(dst, img + 16 * u, (uint32_t)(max(q0, lo) - q0), (uint32_t)(min(span, q0 + 16) - q0));
             }
         }
         __syncthreads();
     }
 }
 
+#ifndef ZR_CMP_HALF
+// 1: the headline compaction in 8-stream groups, 128-lane workgroups (16 per CU):
+// byte-exact, measured slower (0.128 vs 0.115 ms, profiles/r05_ab11.log)
+#define ZR_CMP_HALF 0
+#endif
 #ifndef ZR_CMP_GRID
 #define ZR_CMP_GRID 0  // > 0: the compaction as a grid-stride loop over 256 * ZR_CMP_GRID workgroups
 #endif
-template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_lds(
+template <uint32_t CS, uint32_t CWIN, uint32_t CU_LD, bool IL, int ABL = 0, uint32_t NT = 256>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_enc_compact_lds(
     uint8_t *enc, KArgs a, RansWork w, uint32_t nwin, int has_off) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[sizeof(CmpLds<CS, CWIN>)];
 #if ZR_CMP_GRID
     // grid-stride over the groups' windows (fewer, longer-lived workgroups)
     const uint32_t nv = a.B * w.nblk * (256 / CS) * nwin;
     for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
-        compact_body<CS, CWIN, CU_LD, IL, ABL>(enc, a, w, nwin, has_off, v, smem);
+        compact_body<CS, CWIN, CU_LD, IL, ABL, false, NT>(enc, a, w, nwin, has_off, v, smem);
         __syncthreads();
     }
 #else
-    compact_body<CS, CWIN, CU_LD, IL, ABL>(enc, a, w, nwin, has_off, blockIdx.x, smem);
+    compact_body<CS, CWIN, CU_LD, IL, ABL, false, NT>(enc, a, w, nwin, has_off, blockIdx.x, smem);
 #endif
 }
 
@@ -1855,13 +1879,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             // issues the same number of stores after them
             const uint32_t nunit = (span + 15) / 16;
             const uint32_t u = lane == 0 ? 0 : nunit - 1;
-            if (lane < 2 && nunit && (lane == 0 || nunit > 1) && !(16 * u >= lo && 16 * u + 16 <= span)) {
-                uint8_t *const dst = enc + uoff + 16 * (uint64_t)u;
-                for (uint32_t j = 0; j < 16; j++) {
-                    const uint32_t q = 16 * u + j;
-                    if (q >= lo && q < span) dst[j] = img[q];
-                }
-            }
+            if (lane < 2 && nunit && (lane == 0 || nunit > 1) && !(16 * u >= lo && 16 * u + 16 <= span))
+                unit_range_store(enc + uoff + 16 * (uint64_t)u, img + 16 * u, max(16 * u, lo) - 16 * u,
+                                 min(span, 16 * u + 16) - 16 * u);
         }
         prefetch(gid + G, slot[(k + 1) & 1]);
         if (wv == 0) meta_load(gid + 3 * G);
@@ -4331,6 +4351,13 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             if (wpc && w.il && has_off && w.nblk <= SCAN_FUSE && gp && (gx * 16 + gp - 1) / gp <= CP_MAXK) {
                 // the pipelined compaction: wpc workgroups per CU walk the groups
                 launch_timed("rans_compact", k_enc_compact_pipe, dim3(gp), dim3(256), 0, s, enc, a, w);
+            } else if (ZR_CMP_HALF && w.il && has_off && w.nblk <= SCAN_FUSE) {
+                // 8-stream groups, 128-lane workgroups, 16 per CU
+                constexpr uint32_t CWIN8 = 10240 - (uint32_t)sizeof(CmpLds<8, 0>);
+                static_assert(sizeof(CmpLds<8, CWIN8>) <= 10240 && CWIN8 % 16 == 0, "16 workgroups per CU");
+                const uint32_t nwin8 = (uint32_t)std::max<uint64_t>(1, (8ull * w.cap + 16) / CWIN8 / 2);
+                launch_timed("rans_compact", k_enc_compact_lds<8, CWIN8, 4, true, 0, 128>,
+                             dim3((uint32_t)(gx * 32 * nwin8)), dim3(128), 0, s, enc, a, w, nwin8, has_off);
             } else {
                 launch_timed("rans_compact", kcmp, dim3(gcmp), dim3(256), 0, s, enc, a, w, nwin, has_off);
             }
