@@ -1500,11 +1500,12 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
                 dpos[k] = 0;
                 const uint8_t *src = sbase;
                 if (IL) {
+                    // (IL: the chunk's place is recomputed after the loads, so that
+                    // only the loads' registers are live across them)
                     const uint32_t c = qrow0 + f / CS;
                     if (f < nchunks && (int32_t)c >= mi.x && (int32_t)c < mi.y) {
                         src = scol + c * (IL_SPAN * 16);
-                        dpos[k] = mi.z + 16 * (int32_t)c;
-                        nv[k] = (uint32_t)min(16, mi.w - dpos[k]);
+                        nv[k] = 1;
                     }
                 } else if (f < nchunks) {
                     while (cpre[si + 1] <= f) si++;
@@ -1516,7 +1517,16 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
                 // the scratch is dead once read: non-temporal (profiles/r05_ab3.log, 0.120 -> 0.114 ms)
                 v[k] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>((nv[k] && !(ABL & 4)) ? src : sbase + (lane % CS) * 16));
             }
+            uint32_t lane2 = lane;
+            asm volatile("" : "+v"(lane2));
             for (uint32_t k = 0; k < CU_LD; k++) {
+                if (IL) {
+                    const uint32_t f = f0 + 64 * k + lane2;
+                    const uint32_t c = qrow0 + f / CS;
+                    const bool ok = f < nchunks && (int32_t)c >= mi.x && (int32_t)c < mi.y;
+                    dpos[k] = mi.z + 16 * (int32_t)c;
+                    nv[k] = ok ? (uint32_t)min(16, mi.w - dpos[k]) : 0u;
+                }
                 if (!nv[k]) continue;
                 if (ABL & 2) {
                     asm volatile("" ::"v"(v[k].x), "v"(v[k].w));
@@ -1598,6 +1608,12 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
     }
 }
 
+#ifndef ZR_CMP_LD
+// the interleaved compaction's 16-B loads per lane per round. 5 would take a
+// 65-row group (incompressible 1 KiB streams) in one round instead of two, but
+// spills at 64 VGPRs: 0.143 against 0.114 ms (profiles/r05_ab13.log)
+#define ZR_CMP_LD 4
+#endif
 #ifndef ZR_CMP_HALF
 // 1: the headline compaction in 8-stream groups, 128-lane workgroups (16 per CU):
 // byte-exact, measured slower (0.128 vs 0.115 ms, profiles/r05_ab11.log)
@@ -1903,7 +1919,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     // the groups wider than the window
     for (uint32_t k = 0, gid = g0; gid < ng; k++, gid += G) {
         if (slowm[k / 32] & (1u << (k % 32))) {
-            compact_body<CS, CP_WIN, 4, true>(enc, a, w, 1, 1, gid, smem);
+            compact_body<CS, CP_WIN, ZR_CMP_LD, true>(enc, a, w, 1, 1, gid, smem);
             __syncthreads();
         }
     }
@@ -1927,7 +1943,7 @@ __global__ __launch_bounds__(256) void k_enc_cmp_fused(const uint8_t *raw, uint8
     if (blockIdx.x < nenc)
         enc_xn_body<256, 0, IL>(raw, ahi, whi, blockIdx.x, lds);
     else
-        compact_body<16, CWIN, 4, IL>(enc, alo, wlo, 1, has_off, blockIdx.x - nenc, lds);
+        compact_body<16, CWIN, IL ? ZR_CMP_LD : 4, IL>(enc, alo, wlo, 1, has_off, blockIdx.x - nenc, lds);
 }
 
 // Encode and compaction in ONE launch (zr_rans_set_encode_fused, VERDICT r4
@@ -1959,7 +1975,7 @@ __global__ __launch_bounds__(256) void k_enc_lb(const uint8_t *raw, uint8_t *enc
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (uint32_t g = 0; g < 16; g++) {
-        compact_body<16, CWIN, 4, IL, 0, true>(enc, a, w, 1, 1, L * 16 + g, lds, tag);
+        compact_body<16, CWIN, IL ? ZR_CMP_LD : 4, IL, 0, true>(enc, a, w, 1, 1, L * 16 + g, lds, tag);
         __syncthreads();
     }
     if (threadIdx.x == 0 &&
@@ -4306,7 +4322,7 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             launch_timed("rans_encode_compact", w.il ? k_enc_cmp_fused<true> : k_enc_cmp_fused<false>,
                          dim3(nhi + 16 * nlo), dim3(256), 0, s, raw, enc, ahi, whi, nhi, alo, wlo, 1);
             constexpr uint32_t CWIN = 19 * 1024;
-            launch_timed("rans_compact", w.il ? k_enc_compact_lds<16, CWIN, 4, true> : k_enc_compact_lds<16, CWIN, 4, false>,
+            launch_timed("rans_compact", w.il ? k_enc_compact_lds<16, CWIN, ZR_CMP_LD, true> : k_enc_compact_lds<16, CWIN, 4, false>,
                          dim3(16 * nhi), dim3(256), 0, s, enc, ahi, whi, 1u, 1);
         } else if (!narrow && !wide) {
             launch_timed("rans_encode", kenc, dim3((uint32_t)gx), dim3(256), 0, s, raw, a, w);
@@ -4324,19 +4340,19 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
             const uint32_t nwin = (uint32_t)std::max<uint64_t>(1, max_span / CWIN / 2);
 #ifdef ZR_DIAG
             static const int cabl = getenv("ZR_CMP_ABL") ? atoi(getenv("ZR_CMP_ABL")) : 0;  // profiling only
-            auto kcmp = w.il ? k_enc_compact_lds<16, CWIN, 4, true> : k_enc_compact_lds<16, CWIN, 4, false>;
+            auto kcmp = w.il ? k_enc_compact_lds<16, CWIN, ZR_CMP_LD, true> : k_enc_compact_lds<16, CWIN, 4, false>;
             if (w.il) {
                 switch (cabl) {
-                    case 1: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 1>; break;
-                    case 2: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 2>; break;
-                    case 3: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 3>; break;
-                    case 4: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 4>; break;
-                    case 7: kcmp = k_enc_compact_lds<16, CWIN, 4, true, 7>; break;
+                    case 1: kcmp = k_enc_compact_lds<16, CWIN, ZR_CMP_LD, true, 1>; break;
+                    case 2: kcmp = k_enc_compact_lds<16, CWIN, ZR_CMP_LD, true, 2>; break;
+                    case 3: kcmp = k_enc_compact_lds<16, CWIN, ZR_CMP_LD, true, 3>; break;
+                    case 4: kcmp = k_enc_compact_lds<16, CWIN, ZR_CMP_LD, true, 4>; break;
+                    case 7: kcmp = k_enc_compact_lds<16, CWIN, ZR_CMP_LD, true, 7>; break;
                     default: break;
                 }
             }
 #else
-            auto kcmp = w.il ? k_enc_compact_lds<16, CWIN, 4, true> : k_enc_compact_lds<16, CWIN, 4, false>;
+            auto kcmp = w.il ? k_enc_compact_lds<16, CWIN, ZR_CMP_LD, true> : k_enc_compact_lds<16, CWIN, 4, false>;
 #endif
             // the 256-lane encoder leaves each stream's offset in its block (a
             // block's bytes fit 32 bits: 256 * cap < 2^32)
