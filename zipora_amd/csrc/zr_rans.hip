@@ -46,14 +46,51 @@ __device__ __forceinline__ void st_u32_u(uint8_t *p, uint32_t v) {
     p[3] = (uint8_t)(v >> 24);
 }
 
-__device__ __forceinline__ unsigned long long wave_incl_scan(unsigned long long v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        unsigned long long t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
+// Wave scans and sums by DPP: row shifts within the 16-lane rows, then GFX9's
+// row broadcasts (lane 15 into rows 1 and 3, lane 31 into rows 2 and 3). No
+// LDS round trip on the chain (the __shfl forms are a ds_bpermute per step,
+// two per step for 64-bit values: ~12 dependent LDS round trips per scan).
+// 64-bit values go as four 16-bit pieces, whose 64-lane sums fit 22 bits.
+// Call with the whole wave active.
+__device__ __forceinline__ uint32_t dpp_scan32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return v;
+}
+
+// inclusive max scan of unsigned 32-bit values (0 is the identity)
+__device__ __forceinline__ uint32_t dpp_scan_max32(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+
+// a wave-uniform 64-bit value kept in SGPRs
+__device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+}
+
+// lane l's 64-bit value (l wave-uniform), by two v_readlane: no LDS round trip
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t l) {
+    const int ll = __builtin_amdgcn_readfirstlane((int)l);
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, ll) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), ll) << 32);
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan(unsigned long long v) {
+    const uint32_t a = dpp_scan32((uint32_t)v & 0xFFFF), b = dpp_scan32((uint32_t)v >> 16),
+                   c = dpp_scan32((uint32_t)(v >> 32) & 0xFFFF), d = dpp_scan32((uint32_t)(v >> 48));
+    return (unsigned long long)a + ((unsigned long long)b << 16) + ((unsigned long long)c << 32) +
+           ((unsigned long long)d << 48);
 }
 
 // exclusive scan over a 256-thread block; sh must hold 4 entries
@@ -86,11 +123,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(void *base) {
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(u), 0, 0x7FFFFFFF, 0x00020000);
 }
 
-// sum over one wave (every lane gets it)
+// sum over one wave (every lane gets it): lane 63 of the DPP scan
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor((unsigned long long)v, d, 64);
-    return v;
+    const uint32_t a = dpp_scan32((uint32_t)v & 0xFFFF), b = dpp_scan32((uint32_t)v >> 16),
+                   c = dpp_scan32((uint32_t)(v >> 32) & 0xFFFF), d = dpp_scan32((uint32_t)(v >> 48));
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)a, 63) +
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)b, 63) << 16) +
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)c, 63) << 32) +
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)d, 63) << 48);
 }
 
 __device__ __forceinline__ const RansDTab *tab_for(const void *tables, uint32_t stride, uint32_t b) {
@@ -399,15 +439,10 @@ __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_
         run = max(run, q.z); m[i + 2] = run;
         run = max(run, q.w); m[i + 3] = run;
     }
-    uint32_t inc = run;  // inclusive max over threads <= v
-    for (uint32_t dlt = 1; dlt < 64; dlt <<= 1) {
-        const uint32_t t = __shfl_up(inc, dlt, 64);
-        if ((v & 63) >= dlt) inc = max(inc, t);
-    }
+    const uint32_t inc = dpp_scan_max32(run);  // inclusive max over threads <= v
     if ((v & 63) == 63) wmax[v >> 6] = inc;
     __syncthreads();
-    uint32_t pre = __shfl_up(inc, 1, 64);
-    if ((v & 63) == 0) pre = 0;
+    uint32_t pre = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xF, 0xF, false);  // wave_shr:1 (lane 0: 0)
     for (uint32_t wi = 0; wi < (v >> 6); wi++) pre = max(pre, wmax[wi]);
     v4u *dst = reinterpret_cast<v4u *>(&d->slot[16 * v]);
     for (uint32_t i = 0; i < 16; i += 4) {
@@ -1321,8 +1356,8 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
     // the group's streams: offsets, lengths, header words, first window's chunk
     // ranges (lanes [l0, l0 + ns) of the calling wave hold streams s0 ..)
     auto group_setup = [&](bool mine, uint32_t i, uint32_t sb, uint64_t off, uint32_t L, uint32_t X, uint32_t l0) {
-        const uint64_t g_r0 = __shfl(off, (int)l0, 64);
-        const uint64_t g_r1 = __shfl(off + L, (int)(l0 + ns - 1), 64);
+        const uint64_t g_r0 = lane_u64(off, l0);
+        const uint64_t g_r1 = lane_u64(off + L, l0 + ns - 1);
         const uintptr_t g_ua0 = ((uintptr_t)dbase + g_r0) & ~(uintptr_t)15;
         const uint64_t g_span = (uintptr_t)dbase + g_r1 - g_ua0;
         if (mine) {
@@ -1450,7 +1485,8 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
     }
     uint64_t span = 0;
     uintptr_t ua0 = 0;
-    const uint64_t r0 = soff[0], r1 = soff[ns - 1] + slen[ns - 1];
+    // (the group's extent is workgroup-uniform: in SGPRs, not VGPRs)
+    const uint64_t r0 = uni_u64(soff[0]), r1 = uni_u64(soff[ns - 1] + slen[ns - 1]);
     if (r1 <= r0) return;
     ua0 = ((uintptr_t)dbase + r0) & ~(uintptr_t)15;
     span = (uintptr_t)dbase + r1 - ua0;  // bytes of the image from ua0
@@ -1483,8 +1519,8 @@ __device__ __forceinline__ void compact_body(uint8_t *enc, const KArgs &a, const
         // ---- phase 1: chunks -> LDS image. Stream-major: flat chunk f belongs
         // to stream i with cpre[i] <= f < cpre[i+1]. IL: flat f is quad row
         // crng[0] + f / CS of stream f % CS.
-        const uint32_t nchunks = IL ? (crng[1] > crng[0] ? (crng[1] - crng[0]) * CS : 0u) : cpre[ns];
-        const uint32_t qrow0 = IL ? crng[0] : 0u;
+        const uint32_t nchunks = __builtin_amdgcn_readfirstlane(IL ? (crng[1] > crng[0] ? (crng[1] - crng[0]) * CS : 0u) : cpre[ns]);
+        const uint32_t qrow0 = __builtin_amdgcn_readfirstlane(IL ? crng[0] : 0u);
         // IL: f0 and 64 k are multiples of CS, so a lane's stream is lane % CS
         // for the whole window: its range, once, and its scratch column
         const int4 mi = IL ? ilm[lane % CS] : make_int4(0, 0, 0, 0);
@@ -1767,7 +1803,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                             st_u32_u(e + 8 * (size_t)N + 4 * (size_t)sb, mL);
                         }
                     }
-                    const uint64_t r0 = __shfl(off, 0, 64), r1 = __shfl(off + mL, (int)ns - 1, 64);
+                    const uint64_t r0 = lane_u64(off, 0), r1 = lane_u64(off + mL, ns - 1);
                     if (r1 > r0) {
                         const uint64_t d0 = eoff + 12 * (uint64_t)N;  // the streams' first byte, from enc
                         const uint64_t u0 = (((uintptr_t)enc + d0 + r0) & ~(uintptr_t)15) - (uintptr_t)enc;
