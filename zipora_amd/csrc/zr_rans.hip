@@ -734,17 +734,38 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     constexpr bool V2 = ZR_ENC_V2 != 0 && EW >= 256;
     constexpr bool V2O = V2;
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
-    for (uint32_t i = tid; i < 256 * TC; i += EW) {
-        const uint32_t v = i / TC;
-        const uint32_t f = T->freq[v];
-        if constexpr (V2) {
-            et[i] = enc_entry_v2(f, T->start[v]);
-            continue;
+    // the table's words are loaded here and the entries built after the first
+    // input piece's load is issued: the two share one memory round trip
+    constexpr uint32_t TPT = (256 * TC + EW - 1) / EW;  // table entries per thread
+    uint32_t tf[TPT], ts[TPT], tr[TPT], th[TPT];
+#pragma unroll
+    for (uint32_t j = 0; j < TPT; j++) {
+        const uint32_t i = tid + j * EW, v = i / TC;
+        tf[j] = ts[j] = tr[j] = th[j] = 0;
+        if (i < 256 * TC) {
+            tf[j] = T->freq[v];
+            ts[j] = T->start[v];
+            if constexpr (!V2) {
+                tr[j] = T->rcp[v];
+                th[j] = T->rsh[v];
+            }
         }
-        const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
-        et[i] = make_uint4(f ? t1 | (t2 << 16) : 0u, T->start[v] << 8, T->rcp[v],
-                           (((TOTFREQ - f) & 0xFFF) << 8) | (T->rsh[v] << 24));
     }
+    auto build_table = [&]() {
+#pragma unroll
+        for (uint32_t j = 0; j < TPT; j++) {
+            const uint32_t i = tid + j * EW;
+            if (i >= 256 * TC) continue;
+            const uint32_t f = tf[j];
+            if constexpr (V2) {
+                et[i] = enc_entry_v2(f, ts[j]);
+                continue;
+            }
+            const uint32_t t1 = (f << 4) - 1, t2 = f < 16 ? (f << 12) - 1 : 0xFFFFu;
+            et[i] = make_uint4(f ? t1 | (t2 << 16) : 0u, ts[j] << 8, tr[j],
+                               (((TOTFREQ - f) & 0xFFF) << 8) | (th[j] << 24));
+        }
+    };
     // Input rows k*N + EW*blk .. +EW-1 are staged through the LDS tile of ETILE
     // rows: each thread moves one 16-byte piece per tile (coalesced), loaded into
     // registers one tile ahead (the loads fly while the previous tile is coded).
@@ -984,9 +1005,10 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
         }
     };
     const uint64_t ntiles = (cmax + ETILE - 1) / ETILE;
+    v4u pend = issue_piece(ntiles - 1);
+    build_table();
     if constexpr (V2O) ring[tid] = 0u;  // row 0: the first partial dword
     __syncthreads();  // the encode table
-    v4u pend = issue_piece(ntiles - 1);
     // the tile loop, top tile first. Tiles ntiles-2 .. 1 are full for every
     // stream and their next piece is a plain 16-B load when the workgroup's
     // columns are all streams and the input is 16-B aligned.
