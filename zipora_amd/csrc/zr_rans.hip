@@ -107,6 +107,19 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, unsigned long lo
     return base + inc - v;
 }
 
+// 32-bit exclusive scan over a 256-thread block (wrapping adds); sh: 4 words
+__device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t *sh, uint32_t *total) {
+    const uint32_t inc = dpp_scan32(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) sh[w] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < w; i++) base += sh[i];
+    if (total) *total = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+    return base + inc - v;
+}
+
 __device__ __forceinline__ uint64_t block_sum(uint64_t v, unsigned long long *sh) {
     uint64_t t;
     block_excl_scan(v, sh, &t);
@@ -335,18 +348,28 @@ __global__ __launch_bounds__(256) void k_hist_small(const uint8_t *raw, KArgs a,
 // One 256-thread workgroup builds table d from the raw counts, thread v
 // holding f = count of byte v. pool: LDS scratch of TAB_POOL_WORDS words,
 // 16-B aligned (k_tab's own, or k_hist's histogram copies once summed).
+#ifdef ZR_TAB_STAMPS  // tools/micro/tabcost.hip only: s_memtime at each phase of the build
+__device__ uint64_t *g_tab_stamps;
+#define TAB_STAMP(i) do { __syncthreads(); if (threadIdx.x == 0 && g_tab_stamps) g_tab_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define TAB_STAMP(i) do { } while (0)
+#endif
 __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_t *pool) {
+    TAB_STAMP(0);
     uint32_t *const mark = pool;  // TOTFREQ words (the slot owners below)
     uint32_t *const norm_s = pool + TOTFREQ, *const start_s = norm_s + 256, *const freq_raw = start_s + 256;
     unsigned long long *const sh = reinterpret_cast<unsigned long long *>(freq_raw + 256);  // 4
-    unsigned long long &best = sh[4];
     uint32_t *const wmax = reinterpret_cast<uint32_t *>(sh + 5);  // 4
     const uint32_t v = threadIdx.x;
     freq_raw[v] = f;
     // total_freq: u32 wrapping sum (rans.rs:209), and (bits 48+) the number of
     // present symbols (pass 1, rans.rs:244-250), in one reduction
-    const uint64_t tu = block_sum((uint64_t)f | ((uint64_t)(f > 0) << 48), sh);
-    const uint32_t total = (uint32_t)tu;
+    // (32-bit scans: the total wraps as the reference's u32 sum, rans.rs:209)
+    uint32_t *const sh32 = reinterpret_cast<uint32_t *>(sh);
+    uint32_t total, used;
+    block_excl_scan32(f, sh32, &total);
+    block_excl_scan32(f > 0 ? 1u : 0u, sh32, &used);
+    TAB_STAMP(1);
     if (total == 0) {  // empty encoder (rans.rs:210-216)
         d->freq[v] = 0;
         d->start[v] = 0;
@@ -360,7 +383,7 @@ __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_
         return;
     }
     // pass 1: one slot per present symbol (rans.rs:244-250)
-    const uint32_t used = (uint32_t)(tu >> 48);
+
     const uint64_t ir = TOTFREQ - used;  // initial_remaining (rans.rs:263)
     // pass 2: proportional share of the initial budget (rans.rs:264-271),
     // additional = (f * ir / total) as u32, clamped to the live `remaining`.
@@ -377,24 +400,33 @@ __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_
         q -= q * total > num;
         add_raw = (uint32_t)q;
     }
-    uint64_t tot_raw;
-    const uint64_t pre_add = block_excl_scan(add_raw, sh, &tot_raw);
+    TAB_STAMP(2);
+    // (scanned clamped to ir: min(prefix, ir) and min(total, ir) are unchanged,
+    // and the sums stay below 2^20)
+    uint32_t tot_raw32;
+    const uint64_t pre_add = block_excl_scan32((uint32_t)min((uint64_t)add_raw, ir), sh32, &tot_raw32);
+    const uint64_t tot_raw = tot_raw32;
     const uint32_t add = (uint32_t)min((uint64_t)add_raw, ir - min(pre_add, ir));
     uint32_t norm = (f > 0 ? 1u : 0u) + add;
     // the clamped shares saturate at ir: their sum is min(sum of the raw shares, ir)
     uint32_t remaining = (uint32_t)(ir - min(tot_raw, ir));
     norm_s[v] = norm;
     __syncthreads();
+    TAB_STAMP(3);
     // pass 3 (rans.rs:274-296): +1 to the largest raw freq (lowest index on ties)
     // whose normalised freq is < 1024; repeated +1 on the same argmax is batched.
+    // The argmax by wave maxima (DPP) and four partials, not an LDS atomic max
+    // on one word from 256 lanes (serialised: 45 % of the build,
+    // tools/micro/tabcost.hip): per wave the largest eligible freq, then the
+    // lowest index holding it (as 256 - v); partial = freq << 9 | (256 - v)
+    unsigned long long *const wbest = sh + 4;  // 4 (aliases best and wmax: not live here)
     while (remaining > 0) {
-        if (v == 0) best = 0;
+        const bool elig = f > 0 && norm_s[v] < TOTFREQ / 4;
+        const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)dpp_scan_max32(elig ? f : 0u), 63);
+        const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)dpp_scan_max32(elig && f == m1 ? 256u - v : 0u), 63);
+        if ((v & 63) == 0) wbest[v >> 6] = ((unsigned long long)m1 << 9) | m2;
         __syncthreads();
-        const uint32_t fv = freq_raw[v];
-        if (fv > 0 && norm_s[v] < TOTFREQ / 4)
-            atomicMax(&best, ((unsigned long long)fv << 8) | (255 - v));
-        __syncthreads();
-        const unsigned long long bk = best;
+        const unsigned long long bk = max(max(wbest[0], wbest[1]), max(wbest[2], wbest[3]));
         __syncthreads();
         if (bk == 0) {  // fallback: first non-zero symbol (rans.rs:284-292)
             if (v == 0) {
@@ -406,18 +438,25 @@ __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_
             }
             remaining = 0;
         } else {
-            const uint32_t idx = 255 - (uint32_t)(bk & 0xFF);
+            const uint32_t idx = 256 - (uint32_t)(bk & 0x1FF);
             const uint32_t give = min(remaining, TOTFREQ / 4 - norm_s[idx]);
+            // (every thread has read norm_s[idx] before thread 0 adds to it: without
+            // this barrier a wave behind wave 0 could read the new value and take
+            // another `give`, its `remaining` then differing from the others')
+            __syncthreads();
             if (v == 0) norm_s[idx] += give;
             remaining -= give;
         }
         __syncthreads();
     }
+    TAB_STAMP(4);
     norm = norm_s[v];
-    uint64_t tot;  // (bits 48+: the symbols owning all 4096 slots, i.e. DT_SINGLE)
-    const uint32_t start = (uint32_t)block_excl_scan((uint64_t)norm | ((uint64_t)(norm == TOTFREQ) << 48), sh, &tot);
-    const uint32_t maxn = (uint32_t)(tot >> 48);
-    start_s[v] = start;
+    uint32_t tot;  // (bits 20+: the symbols owning all 4096 slots, i.e. DT_SINGLE)
+    const uint32_t start = block_excl_scan32(norm | ((norm == TOTFREQ ? 1u : 0u) << 20), sh32, &tot) & 0xFFFFF;
+    const uint32_t maxn = tot >> 20;
+    // start_s: the symbol's slot-entry base, v | f << 20 (f < 4096) minus its start
+    // << 8, so the entry of its slot j is base + (j << 8) (one LDS read a slot)
+    start_s[v] = v + ((norm < TOTFREQ ? norm : 0u) << 20) - (start << 8);
     d->freq[v] = norm;
     d->start[v] = start;
     d->rsh[v] = enc_rsh(norm);
@@ -426,7 +465,8 @@ __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_
     // 4096 slots (thread v owns slots 16v..16v+15); zero-frequency symbols
     // share the next start and are never marked, so the owner of slot j is
     // the last present symbol with start <= j
-    for (uint32_t j = v; j < TOTFREQ; j += 256) mark[j] = 0;
+    TAB_STAMP(5);
+    for (uint32_t j = v; j < TOTFREQ / 4; j += 256) reinterpret_cast<v4u *>(mark)[j] = v4u{0, 0, 0, 0};
     __syncthreads();
     if (norm > 0) mark[start] = v + 1;
     __syncthreads();
@@ -444,14 +484,14 @@ __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_
     __syncthreads();
     uint32_t pre = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xF, 0xF, false);  // wave_shr:1 (lane 0: 0)
     for (uint32_t wi = 0; wi < (v >> 6); wi++) pre = max(pre, wmax[wi]);
+    TAB_STAMP(6);
     v4u *dst = reinterpret_cast<v4u *>(&d->slot[16 * v]);
     for (uint32_t i = 0; i < 16; i += 4) {
         uint32_t o[4];
         for (uint32_t k = 0; k < 4; k++) {
             const uint32_t own = max(pre, m[i + k]) - 1;
             const uint32_t j = 16 * v + i + k;
-            const uint32_t fs = norm_s[own];
-            o[k] = own | ((j - start_s[own]) << 8) | ((fs < TOTFREQ ? fs : 0u) << 20);
+            o[k] = start_s[own] + (j << 8);  // own | (j - start) << 8 | f << 20
         }
         dst[i >> 2] = v4u{o[0], o[1], o[2], o[3]};
     }
@@ -459,8 +499,17 @@ __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_
         d->kind = maxn ? DT_SINGLE : DT_NORMAL;
         d->status = ZR_OK;
     }
+    TAB_STAMP(7);
 }
 
+#ifdef ZR_TAB_STAMPS
+__global__ __launch_bounds__(256) void k_tab_stamped(const uint32_t *hist, RansDTab *tabs, uint64_t *stamps) {
+    __shared__ __attribute__((aligned(16))) uint32_t pool[TAB_POOL_WORDS];
+    if (threadIdx.x == 0) g_tab_stamps = stamps;
+    __syncthreads();
+    tab_build(hist[threadIdx.x], tabs, pool);
+}
+#endif
 // clear: non-null = the histogram itself, zeroed once read (each thread its own
 // bin), so the next accumulating zr_histogram_dev needs no memset
 __global__ __launch_bounds__(256) void k_tab(const uint32_t *hist, RansDTab *tabs, uint32_t *clear) {
