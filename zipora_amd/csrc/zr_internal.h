@@ -75,15 +75,23 @@ __host__ __device__ inline uint32_t enc_rsh(uint32_t f) { return f <= 1 ? 0u : 3
 __host__ __device__ inline uint32_t enc_rcp(uint32_t f) {
     return f ? (uint32_t)(((1ull << (24 + enc_rsh(f))) + f - 1) / f) : 0u;
 }
-// enc_rcp without a 64-bit division (device table builds): the quotient of
-// the exact doubles 2^(24 + rsh) + f - 1 (< 2^37) and f, truncated, then
-// corrected to the floor (the rounded quotient is at most one above it)
+// enc_rcp without a 64-bit division (device table builds)
+// floor(num / d) for num < 2^53, d >= 1: the f64 reciprocal (v_rcp_f64 and one
+// Newton step) gives a quotient within one of the floor either way, corrected
+// by the remainder's sign and size (no IEEE division sequence on the chain)
+__device__ inline uint64_t floor_div_u64(uint64_t num, uint32_t d) {
+    const double dd = (double)d;
+    double r = __builtin_amdgcn_rcp(dd);
+    r = __builtin_fma(__builtin_fma(-dd, r, 1.0), r, r);
+    uint64_t q = (uint64_t)((double)num * r);
+    const int64_t rem = (int64_t)(num - q * d);
+    q += rem >= (int64_t)d ? 1 : 0;
+    q -= rem < 0 ? 1 : 0;
+    return q;
+}
 __device__ inline uint32_t enc_rcp_fast(uint32_t f) {
     if (!f) return 0u;
-    const uint64_t num = (1ull << (24 + enc_rsh(f))) + f - 1;
-    uint64_t q = (uint64_t)((double)num / (double)f);
-    q -= q * f > num;
-    return (uint32_t)q;
+    return (uint32_t)floor_div_u64((1ull << (24 + enc_rsh(f))) + f - 1, f);
 }
 __host__ __device__ inline uint32_t enc_div(uint32_t x, uint32_t rcp, uint32_t rsh) {
     return (uint32_t)(((uint64_t)(x << 8) * rcp) >> 32) >> rsh;

@@ -391,14 +391,10 @@ __device__ __forceinline__ void tab_build(const uint32_t f, RansDTab *d, uint32_
     // P_v the exclusive prefix sum of the unclamped shares (once it hits 0 it
     // stays 0), so to_add_v = min(add_v, ir - min(P_v, ir)). The clamp binds
     // when the u32 total of rans.rs:209 has wrapped (sum of counts >= 2^32).
-    // (f * ir < 2^44 and total are exact doubles; the quotient rounded to
-    // nearest is at most one above the floor: one correction, no u64 division)
+    // (f * ir < 2^44: floor_div_u64, exact, no u64 or IEEE f64 division)
     uint32_t add_raw = 0;
     if (f > 0) {
-        const uint64_t num = (uint64_t)f * ir;
-        uint64_t q = (uint64_t)((double)num / (double)total);
-        q -= q * total > num;
-        add_raw = (uint32_t)q;
+        add_raw = (uint32_t)floor_div_u64((uint64_t)f * ir, total);
     }
     TAB_STAMP(2);
     // (scanned clamped to ir: min(prefix, ir) and min(total, ir) are unchanged,
