@@ -595,6 +595,9 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 // workgroups (16 waves) per CU.
 // IL: the batch's scratch layout (RansWork::il), a template parameter so that
 // the long-stream (contiguous) instance keeps its constant addressing.
+#ifndef ZR_ENC_TC256
+#define ZR_ENC_TC256 4
+#endif
 #ifndef ZR_ENC_DB
 #define ZR_ENC_DB 1
 #endif
@@ -706,7 +709,7 @@ __device__ __forceinline__ uint32_t enc_step_v2(uint32_t &X, const uint4 e, uint
 // LDS bytes of k_enc_xn's workgroup (ring | encode table | input tiles)
 template <uint32_t EW>
 constexpr uint32_t enc_xn_lds_bytes() {
-    return (ZR_ENC_DB != 0 ? 16u : 32u) * EW * 4 + 256u * 16 * (EW == 1024 ? 16u : 1u) + (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
+    return (ZR_ENC_DB != 0 ? 16u : 32u) * EW * 4 + 256u * 16 * (EW == 1024 ? 16u : EW == 256 ? (uint32_t)ZR_ENC_TC256 : 1u) + (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
 }
 // the encoder of workgroup vblk (its blockIdx.x in k_enc_xn; k_enc_cmp_fused
 // runs it beside the compaction of other buffers), LDS from the caller
@@ -731,8 +734,12 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     // ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and +32) read 16 different bank
     // quads: no bank conflicts, whatever the symbols (one copy: 16 random
     // entries over 16 quads, ~7.7 extra LDS cycles per wave-step). 64 KiB ring +
-    // 64 KiB table + 32 KiB tiles = the CU's 160 KiB.
-    constexpr uint32_t TC = EW == 1024 ? 16 : 1;
+    // 64 KiB table + 32 KiB tiles = the CU's 160 KiB. The 256-lane shape keeps
+    // ZR_ENC_TC256 = 4 (lane l reads copy l & 3: a lane group's 16 reads fall in
+    // 4 disjoint sets of 4 quads): 40 KiB per workgroup, 4 per CU (5 with one
+    // copy), encoder 0.1629 -> 0.1609 ms, step 0.4795 -> 0.4783 ms, 5 rounds
+    // (profiles/r05_ab19_tc.log; 2 copies: no gain).
+    constexpr uint32_t TC = EW == 1024 ? 16 : EW == 256 ? ZR_ENC_TC256 : 1;
     // (A linear output buffer of ERS + 1 rows re-based at each flush, so that
     // the overflow row is an immediate offset with no wrap: 2 VALU fewer per
     // step pair, but the row move at each flush put an LDS read -> write
