@@ -1003,7 +1003,7 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     // PF: the tile's 16 symbols are read first and each group's four table
     // entries one group ahead, so the two dependent LDS round trips (symbol,
     // then entry) of a group overlap the previous group's coding
-    auto tile_fast_pf = [&](const uint8_t *tl) {
+    auto tile_fast_pf = [&](const uint8_t *tl, auto chk) {
         uint32_t sy[ETILE];
 #pragma unroll
         for (int r = 0; r < (int)ETILE; r++) sy[r] = tl[r * EW + tid];
@@ -1017,8 +1017,10 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
                 n1 = ent(sy[g - 3]);
                 n0 = ent(sy[g - 4]);
             }
-            xmin = min(min(xmin, c3.x), c2.x);  // two v_min3 per group
-            xmin = min(min(xmin, c1.x), c0.x);
+            if constexpr (decltype(chk)::value) {
+                xmin = min(min(xmin, c3.x), c2.x);  // two v_min3 per group
+                xmin = min(min(xmin, c1.x), c0.x);
+            }
             uint32_t m3, m2, m1, m0;
             const uint32_t b3 = enc(c3, true, m3);
             const uint32_t b2 = enc(c2, true, m2);
@@ -1030,9 +1032,9 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
             if (g == ETILE - 4) flush_store();
         }
     };
-    auto tile_fast = [&](const uint8_t *tl) {
+    auto tile_fast = [&](const uint8_t *tl, auto chk) {
         if constexpr (ZR_ENC_PF != 0 && EW == 1024 && !(ABL & 2)) {  // (256 lanes: measured no gain)
-            tile_fast_pf(tl);
+            tile_fast_pf(tl, chk);
             return;
         }
 #pragma unroll
@@ -1044,8 +1046,10 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
                 s3 = s2 = s1 = s0 = t;
             }
             const uint4 e3 = ent(s3), e2 = ent(s2), e1 = ent(s1), e0 = ent(s0);
-            xmin = min(min(xmin, e3.x), e2.x);  // two v_min3 per group
-            xmin = min(min(xmin, e1.x), e0.x);
+            if constexpr (decltype(chk)::value) {
+                xmin = min(min(xmin, e3.x), e2.x);  // two v_min3 per group
+                xmin = min(min(xmin, e1.x), e0.x);
+            }
             uint32_t n3, n2, n1, n0;
             const uint32_t b3 = enc(e3, true, n3);
             const uint32_t b2 = enc(e2, true, n2);
@@ -1060,7 +1064,29 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     v4u pend = issue_piece(ntiles - 1);
     build_table();
     if constexpr (V2O) ring[tid] = 0u;  // row 0: the first partial dword
+    // FULL: every one of the 256 symbols has a frequency, so no coded symbol can
+    // be missing from the table and the full tiles skip the check (two v_min3
+    // per four steps; the check removed outright: encoder 0.1616 -> 0.1566 ms,
+    // profiles/r05_ab20_xmin.log; this form, 81 VGPRs with both tile bodies:
+    // 0.1661 -> 0.1622 ms, step 0.4844 -> 0.4798 ms, r05_ab21_full.log).
+    // Each wave's "some symbol missing" goes to ring row ERS - 1, which no lane
+    // writes before its first tile is coded, behind the first tile barrier
+    // (a tile adds at most 8 rows)
+    {
+        bool miss = false;
+#pragma unroll
+        for (uint32_t j = 0; j < TPT; j++) miss |= tid + j * EW < 256 * TC && tf[j] == 0;
+        const bool wmiss = __builtin_amdgcn_ballot_w64(miss) != 0;
+        if ((tid & 63) == 0) ring[(ERS - 1) * EW + (tid >> 6)] = wmiss ? 1u : 0u;
+    }
     __syncthreads();  // the encode table
+    bool full;
+    {
+        uint32_t m = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < EW / 64; i++) m |= ring[(ERS - 1) * EW + i];
+        full = __builtin_amdgcn_readfirstlane(m) == 0;
+    }
     // the tile loop, top tile first. Tiles ntiles-2 .. 1 are full for every
     // stream and their next piece is a plain 16-B load when the workgroup's
     // columns are all streams and the input is 16-B aligned.
@@ -1106,7 +1132,10 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
         flush_read();
         if (!ZR_ENC_FD) flush_store();
         if (t < tfast && wave_all) {
-            tile_fast(tl);
+            if (full)
+                tile_fast(tl, std::false_type{});
+            else
+                tile_fast(tl, std::true_type{});
         } else {
             flush_store();
             const uint32_t rtop = (uint32_t)min((uint64_t)ETILE, cmax - (uint64_t)t * ETILE);
