@@ -598,6 +598,9 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 #ifndef ZR_ENC_TC256
 #define ZR_ENC_TC256 4
 #endif
+#ifndef ZR_ENC_GUARD
+#define ZR_ENC_GUARD 0
+#endif
 #ifndef ZR_ENC_DB
 #define ZR_ENC_DB 1
 #endif
@@ -709,7 +712,8 @@ __device__ __forceinline__ uint32_t enc_step_v2(uint32_t &X, const uint4 e, uint
 // LDS bytes of k_enc_xn's workgroup (ring | encode table | input tiles)
 template <uint32_t EW>
 constexpr uint32_t enc_xn_lds_bytes() {
-    return (ZR_ENC_DB != 0 ? 16u : 32u) * EW * 4 + 256u * 16 * (EW == 1024 ? 16u : EW == 256 ? (uint32_t)ZR_ENC_TC256 : 1u) + (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
+    return (ZR_ENC_DB != 0 ? 16u : 32u) * EW * 4 + (ZR_ENC_GUARD != 0 && ZR_ENC_V2 != 0 && EW == 256 ? EW * 4 : 0u) +
+           256u * 16 * (EW == 1024 ? 16u : EW == 256 ? (uint32_t)ZR_ENC_TC256 : 1u) + (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
 }
 // the encoder of workgroup vblk (its blockIdx.x in k_enc_xn; k_enc_cmp_fused
 // runs it beside the compaction of other buffers), LDS from the caller
@@ -745,13 +749,28 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     // step pair, but the row move at each flush put an LDS read -> write
     // round trip on the wave: encoder 0.164 -> 0.173 ms, record encoder
     // 0.675 -> 0.688 ms. Dropped.)
-    constexpr uint32_t RING_ALLOC = RING_BYTES;
+    constexpr bool V2 = ZR_ENC_V2 != 0 && EW >= 256;
+    // GD (ZR_ENC_GUARD, the 256-lane V2 shape): a guard row after the ring
+    // takes the overflow of a pair whose low dword is in the last row, so the
+    // overflow's address is the low one + ROW with no wrap (an immediate
+    // offset: two VALU fewer per step pair). Row 0's complete content is then
+    // its own ORs plus the guard: folded in (ds_or) when rows ERS/2.. are
+    // flushed, by which time the pair that crossed into row 0 has written the
+    // guard and the next crossing has not (<= 15 rows pending); row 0 is
+    // cleared when rows 0.. are flushed, its next writer being the ORs after
+    // the next wrap. Measured (profiles/r05_ab23_guard.log, all rANS GPU tests
+    // green): 16 VALU fewer per 16-step tile, but the guard row needs 3 table
+    // copies to keep 4 workgroups per CU (4 copies + guard: 41 KiB, 3 per CU,
+    // encoder 0.181 ms), and 3 copies cost more than the guard saves (0.1653
+    // against 0.1595 ms for 4 copies without it). Off by default
+    constexpr bool GD = ZR_ENC_GUARD != 0 && V2 && EW == 256;
+    constexpr uint32_t RING_ALLOC = RING_BYTES + (GD ? EW * 4 : 0u);
     static_assert(enc_xn_lds_bytes<EW>() == RING_ALLOC + 256 * 16 * TC + (DB ? 2 : 1) * ETILE * EW, "LDS layout");
     uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
     uint4 *et = reinterpret_cast<uint4 *>(lds + RING_ALLOC);
     uint8_t *itile = lds + RING_ALLOC + 256 * 16 * TC;
     // this lane's copy, as the byte offset of entry 0 (entry v: + v * 16 * TC)
-    const uint32_t et_lane = (threadIdx.x & (TC - 1)) * 16;
+    const uint32_t et_lane = (threadIdx.x % TC) * 16;
     auto ent = [&](uint32_t sym) -> const uint4 & {
         return *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(et) + sym * (16 * TC) + et_lane);
     };
@@ -783,7 +802,6 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     // with a lone wave per SIMD (EW = 64, the long-stream shape) every
     // instruction's latency is on the chain and V2 measured slower (literal
     // encode 4.22 -> 4.31 ms; the V2 step alone 4.37 ms, same box)
-    constexpr bool V2 = ZR_ENC_V2 != 0 && EW >= 256;
     constexpr bool V2O = V2;
     const RansDTab *T = tab_for(a.tables, a.table_stride, b);
     // the table's words are loaded here and the entries built after the first
@@ -920,7 +938,7 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
             asm("v_lshlrev_b32 %0, %1, %2\n\tv_and_or_b32 %0, %0, %3, %4"
                 : "=&v"(alo)
                 : "i"(__builtin_ctz(ROW) - 5), "v"(P), "s"((RING_BYTES - 1) & ~(ROW - 1)), "v"(tid * 4));
-            ahi = (alo + ROW) & (RING_BYTES - 1);
+            ahi = GD ? alo + ROW : (alo + ROW) & (RING_BYTES - 1);
             __hip_atomic_fetch_or(static_cast<uint32_t *>(__builtin_assume_aligned(lds + alo, 4)), (uint32_t)v, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_WORKGROUP);
             *reinterpret_cast<uint32_t *>(lds + ahi) = (uint32_t)(v >> 32);
@@ -968,6 +986,13 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
             const uint32_t *r = ring + (nfl & FL) * EW + tid;
 #pragma unroll
             for (int i = 0; i < (int)FL; i++) fd[i] = r[i * EW];
+            if constexpr (GD) {
+                static_assert(2 * FL == ERS, "GD: two flush halves");
+                if (nfl & FL)  // fold the guard into row 0 (the next wrap's ORs are there)
+                    __hip_atomic_fetch_or(ring + tid, ring[ERS * EW + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else  // row 0 read: cleared for the next wrap
+                    ring[tid] = 0u;
+            }
             fo = nfl >> 2;
             nfl += FL;
             flim += FL * 32;
@@ -1033,7 +1058,8 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
         }
     };
     auto tile_fast = [&](const uint8_t *tl, auto chk) {
-        if constexpr (ZR_ENC_PF != 0 && EW == 1024 && !(ABL & 2)) {  // (256 lanes: measured no gain)
+        // (256 lanes: measured slower, 0.161 -> 0.170 ms, profiles/r05_ab24_pf256.log)
+        if constexpr (ZR_ENC_PF != 0 && EW == 1024 && !(ABL & 2)) {
             tile_fast_pf(tl, chk);
             return;
         }
@@ -1064,6 +1090,7 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     v4u pend = issue_piece(ntiles - 1);
     build_table();
     if constexpr (V2O) ring[tid] = 0u;  // row 0: the first partial dword
+    if constexpr (GD) ring[ERS * EW + tid] = 0u;
     // FULL: every one of the 256 symbols has a frequency, so no coded symbol can
     // be missing from the table and the full tiles skip the check (two v_min3
     // per four steps; the check removed outright: encoder 0.1616 -> 0.1566 ms,
@@ -1169,6 +1196,14 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     // the partial dword (its nacc / 8 whole bytes count)
     const uint32_t nw = nw_of();
     auto rrow = [&](uint32_t d) -> uint32_t { return d & (ERS - 1); };
+    // GD: a row 0 pending after rows FL.. (the wrap not yet folded in by their
+    // flush) takes the guard; a row 0 pending first was folded at the flush
+    // before (or is the stream's first row), and the guard may already hold
+    // the next wrap's carry
+    if constexpr (GD) {
+        if ((nfl & (ERS - 1)) == FL && nw - nfl + ((P & 31) ? 1u : 0u) > FL)
+            __hip_atomic_fetch_or(ring + tid, ring[ERS * EW + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     {
         const uint32_t *r = ring + tid;
         while (nw - nfl >= 4) {
