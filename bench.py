@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--pipeline", action="store_true",
                    help="rans: two distinct batches alternate; each step codes one (encode -> decode on the "
                         "main stream) while the histogram + table of the next one run on a second stream")
-    p.add_argument("--enc-width", type=int, default=256, choices=[256, 1024],
+    p.add_argument("--enc-width", type=int, default=256, choices=[256, 512, 1024],
                    help="rans: the xN encoder's workgroup width (zr_rans_set_encoder_width)")
     p.add_argument("--dec-ring", type=int, default=0, choices=[0, 1, 2],
                    help="rans: the xN decoder's ring (zr_rans_set_decoder_ring): 0 auto, 1 VGPR-staged "

@@ -46,7 +46,7 @@ def _kinds(n, b):
     return bytes(np.random.default_rng(b).integers(0, 256, n, dtype=np.uint8))
 
 
-@pytest.mark.parametrize("width,N", [(256, 4096), (256, 1000), (1024, 4096)])
+@pytest.mark.parametrize("width,N", [(256, 4096), (256, 1000), (1024, 4096), (512, 4096), (512, 1536)])
 def test_v2_edge_frequencies_xn(zr, oracle, enc_width, width, N):
     import torch
     from zipora_amd.device import RansDeviceBatch
@@ -99,7 +99,7 @@ def test_v2_edge_frequencies_records(zr, oracle):
     assert torch.equal(out, raw)
 
 
-@pytest.mark.parametrize("width", [256, 1024])
+@pytest.mark.parametrize("width", [256, 512, 1024])
 def test_v2_symbol_missing_from_table(zr, oracle, enc_width, width):
     """A buffer coded with another buffer's table (a byte with f = 0) reports
     "Symbol {} not in frequency table" (rans.rs:311-316) as ZR_INVALID_INPUT."""

@@ -601,6 +601,12 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 #ifndef ZR_ENC_GUARD
 #define ZR_ENC_GUARD 0
 #endif
+#ifndef ZR_ENC_TC512
+#define ZR_ENC_TC512 8
+#endif
+#ifndef ZR_ENC_PF512
+#define ZR_ENC_PF512 0
+#endif
 #ifndef ZR_ENC_DB
 #define ZR_ENC_DB 1
 #endif
@@ -610,7 +616,7 @@ static std::atomic<uint32_t> g_enc_width{256};
 #ifndef ZR_ENC_SPLIT_DEFAULT
 #define ZR_ENC_SPLIT_DEFAULT 0
 #endif
-static bool enc_w1024() { return g_enc_width.load(std::memory_order_relaxed) == 1024; }
+static uint32_t enc_width() { return g_enc_width.load(std::memory_order_relaxed); }
 // the xN decoder's ring for batches of more than 2^16 streams: 0 auto and 1:
 // the VGPR-staged ring (k_dec_xn_fast), 2: the LDS-DMA ring (k_dec_xn_dma, 8
 // waves per SIMD; zr_rans_set_decoder_ring). Round 5 measured the DMA ring
@@ -713,7 +719,7 @@ __device__ __forceinline__ uint32_t enc_step_v2(uint32_t &X, const uint4 e, uint
 template <uint32_t EW>
 constexpr uint32_t enc_xn_lds_bytes() {
     return (ZR_ENC_DB != 0 ? 16u : 32u) * EW * 4 + (ZR_ENC_GUARD != 0 && ZR_ENC_V2 != 0 && EW == 256 ? EW * 4 : 0u) +
-           256u * 16 * (EW == 1024 ? 16u : EW == 256 ? (uint32_t)ZR_ENC_TC256 : 1u) + (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
+           256u * 16 * (EW == 1024 ? 16u : EW == 512 ? (uint32_t)ZR_ENC_TC512 : EW == 256 ? (uint32_t)ZR_ENC_TC256 : 1u) + (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
 }
 // the encoder of workgroup vblk (its blockIdx.x in k_enc_xn; k_enc_cmp_fused
 // runs it beside the compaction of other buffers), LDS from the caller
@@ -743,7 +749,7 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     // 4 disjoint sets of 4 quads): 40 KiB per workgroup, 4 per CU (5 with one
     // copy), encoder 0.1629 -> 0.1609 ms, step 0.4795 -> 0.4783 ms, 5 rounds
     // (profiles/r05_ab19_tc.log; 2 copies: no gain).
-    constexpr uint32_t TC = EW == 1024 ? 16 : EW == 256 ? ZR_ENC_TC256 : 1;
+    constexpr uint32_t TC = EW == 1024 ? 16 : EW == 512 ? ZR_ENC_TC512 : EW == 256 ? ZR_ENC_TC256 : 1;
     // (A linear output buffer of ERS + 1 rows re-based at each flush, so that
     // the overflow row is an immediate offset with no wrap: 2 VALU fewer per
     // step pair, but the row move at each flush put an LDS read -> write
@@ -1059,7 +1065,7 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     };
     auto tile_fast = [&](const uint8_t *tl, auto chk) {
         // (256 lanes: measured slower, 0.161 -> 0.170 ms, profiles/r05_ab24_pf256.log)
-        if constexpr (ZR_ENC_PF != 0 && EW == 1024 && !(ABL & 2)) {
+        if constexpr (ZR_ENC_PF != 0 && (EW == 1024 || (EW == 512 && ZR_ENC_PF512 != 0)) && !(ABL & 2)) {
             tile_fast_pf(tl, chk);
             return;
         }
@@ -4243,7 +4249,8 @@ size_t zr_rans_dtab_bytes(void) { return sizeof(RansDTab); }
 
 int32_t zr_rans_set_encoder_width(uint32_t lanes) {
     clear_error();
-    if (lanes != 256 && lanes != 1024) return set_error(ZR_INVALID_INPUT, "encoder width must be 256 or 1024");
+    if (lanes != 256 && lanes != 512 && lanes != 1024)
+        return set_error(ZR_INVALID_INPUT, "encoder width must be 256, 512 or 1024");
     g_enc_width.store(lanes, std::memory_order_relaxed);
     return ZR_OK;
 }
@@ -4463,13 +4470,17 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
         // round 4 at -3 % encoder time but +13 % in the
         // compaction that follows, so the 256-lane shape stays the default and
         // zr_rans_set_encoder_width(1024) selects the other
-        const bool wide = enc_w1024() && !narrow && a.N % 1024 == 0;
+        const uint32_t ew = enc_width();
+        const bool wide = ew > 256 && !narrow && a.N % ew == 0;
         if (narrow)
             launch_timed("rans_encode", w.il ? k_enc_xn<64, 0, true> : k_enc_xn<64, 0, false>,
                          dim3((uint32_t)round_up(ceil_div(a.N, 64) * a.B, 16)), dim3(64), 0, s, raw, a, w);
-        else if (wide)
+        else if (wide && ew == 1024)
             launch_timed("rans_encode", w.il ? k_enc_xn<1024, 0, true> : k_enc_xn<1024, 0, false>,
                          dim3((uint32_t)(a.N / 1024 * a.B)), dim3(1024), 0, s, raw, a, w);
+        else if (wide)
+            launch_timed("rans_encode", w.il ? k_enc_xn<512, 0, true> : k_enc_xn<512, 0, false>,
+                         dim3((uint32_t)(a.N / 512 * a.B)), dim3(512), 0, s, raw, a, w);
         // split (256-lane shape, one window per group, offsets from the
         // encoder, halves of >= 2^17 streams): see g_enc_split
         const uint32_t sq = (uint32_t)g_enc_split.load(std::memory_order_relaxed);  // the lower part, in quarters
