@@ -49,8 +49,8 @@ def parse():
     p.add_argument("--pipeline", action="store_true",
                    help="rans: two distinct batches alternate; each step codes one (encode -> decode on the "
                         "main stream) while the histogram + table of the next one run on a second stream")
-    p.add_argument("--enc-width", type=int, default=256, choices=[256, 512, 1024],
-                   help="rans: the xN encoder's workgroup width (zr_rans_set_encoder_width)")
+    p.add_argument("--enc-width", type=int, default=0, choices=[0, 256, 512, 1024],
+                   help="rans: the xN encoder's workgroup width (zr_rans_set_encoder_width; 0: the library's default)")
     p.add_argument("--dec-ring", type=int, default=0, choices=[0, 1, 2],
                    help="rans: the xN decoder's ring (zr_rans_set_decoder_ring): 0 auto, 1 VGPR-staged "
                         "(k_dec_xn_fast), 2 LDS-DMA chunks (k_dec_xn_dma, 8 waves per SIMD)")
@@ -891,6 +891,8 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
                                 f"{B} x {n >> 20} MiB buffers, {N}-way interleaved streams each "
                                 f"({B * N} streams), shared table (histogram all-reduce over ranks)"),
                    "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}",
+                   "encoder_lanes": (64 if B * N <= 1 << 16 else ew if N % (ew := int(L.zr_rans_get_encoder_width())) == 0
+                                     else 256),
                    **({"encode_schedule": f"split at buffer {h}: encoder(0..{h}) -> encoder({h}..{B}) + "
                                           f"compaction(0..{h}) in one dispatch -> compaction({h}..{B})"}
                       if split else {}),
@@ -1082,8 +1084,10 @@ def main():
     import zipora_amd as zr
     L = zr.load()
     L.zr_set_device(local)
-    if hasattr(L, "zr_rans_set_encoder_width") and L.zr_rans_set_encoder_width(args.enc_width):
-        raise SystemExit(f"encoder width {args.enc_width} refused")
+    # the split and fused encodes are forms of the 256-lane encoder shape
+    ew = args.enc_width or (256 if args.enc_fused or args.enc_split else 0)
+    if ew and L.zr_rans_set_encoder_width(ew):
+        raise SystemExit(f"encoder width {ew} refused")
     if args.dec_ring and L.zr_rans_set_decoder_ring(args.dec_ring):
         raise SystemExit(f"decoder ring {args.dec_ring} refused")
     if args.enc_fused is not None and L.zr_rans_set_encode_fused(args.enc_fused):

@@ -196,10 +196,13 @@ int32_t zr_rans_set_compact_pipe(int32_t wg_per_cu);
 const char *zr_rans_decoder_kernel(uint32_t n_buffers, uint32_t n_streams);
 /* Tuning (no reference counterpart): the workgroup width of the xN encoder for
  * batches of more than 2^16 streams, process-wide: 256 (default; 4 copies of
- * the encode table, 4 workgroups per CU), 512 (8 copies, 2 per CU) or 1024
- * (one workgroup per CU with 16 conflict-free copies); 512 and 1024 are used
- * where n_streams is a multiple of the width. Output bytes are identical. */
+ * the encode table, 4 workgroups per CU), 512 (8 copies, 2 per CU) or 1024 (one
+ * workgroup per CU with 16 conflict-free copies); 512 and 1024 are used where
+ * n_streams is a multiple of the width, 256 otherwise. The split and fused
+ * encodes (below) apply to the 256-lane shape. Output bytes are identical. */
 int32_t zr_rans_set_encoder_width(uint32_t lanes);
+/* the current setting of zr_rans_set_encoder_width */
+uint32_t zr_rans_get_encoder_width(void);
 /* Tuning (no reference counterpart), process-wide: q = 1..3 codes the xN encode
  * of a batch of at least 2^18 streams (256-lane encoder) as the encoder of the
  * first round(B * q / 4) buffers, then the other buffers' encoder and the first

@@ -12,10 +12,12 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture
 def fused(zr):
     L = zr.load()
-    was = L.zr_rans_get_encode_fused()
+    was, was_w = L.zr_rans_get_encode_fused(), L.zr_rans_get_encoder_width()
+    assert L.zr_rans_set_encoder_width(256) == 0  # (a form of the 256-lane encoder)
     assert L.zr_rans_set_encode_fused(1) == 0
     yield
     L.zr_rans_set_encode_fused(was)
+    L.zr_rans_set_encoder_width(was_w)
 
 
 def _roundtrip(zr, oracle, datas, N, shared=True):

@@ -16,13 +16,15 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture
 def split(zr):
     L = zr.load()
-    was = L.zr_rans_get_encode_split()
+    was, was_w = L.zr_rans_get_encode_split(), L.zr_rans_get_encoder_width()
+    assert L.zr_rans_set_encoder_width(256) == 0  # (a form of the 256-lane encoder)
 
     def set_s(q):
         assert L.zr_rans_set_encode_split(q) == 0
 
     yield set_s
     L.zr_rans_set_encode_split(was)
+    L.zr_rans_set_encoder_width(was_w)
 
 
 def _fill(bt, datas):

@@ -25,8 +25,9 @@ def enc_width(zr):
     def set_w(n):
         assert L.zr_rans_set_encoder_width(n) == 0
 
+    was = L.zr_rans_get_encoder_width()
     yield set_w
-    L.zr_rans_set_encoder_width(256)
+    L.zr_rans_set_encoder_width(was)
 
 
 def _fill(bt, datas):

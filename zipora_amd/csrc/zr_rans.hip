@@ -611,8 +611,17 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 #define ZR_ENC_DB 1
 #endif
 // the xN encoder's workgroup width for batches of more than 2^16 streams
-// (zr_rans_set_encoder_width: 256, the default, or 1024 where N % 1024 == 0)
-static std::atomic<uint32_t> g_enc_width{256};
+// (zr_rans_set_encoder_width: 256, the default, 512 or 1024; 512 and 1024
+// where N is a multiple of the width, else 256). Round 5, whole step, same
+// box: the 1024-lane shape (16 conflict-free table copies, encoder 2-4 %
+// faster) 0.3 % and 0.6 % faster on two boxes and 0.3 % slower on a third
+// (its compaction 1.5 % slower there), the 512-lane shape (8 copies) 1 %
+// slower (profiles/r05_ab25_width.log, r05_ab26_width.log): within noise of
+// each other, so the long-tested 256-lane shape stays the default
+#ifndef ZR_ENC_WIDTH_DEFAULT
+#define ZR_ENC_WIDTH_DEFAULT 256
+#endif
+static std::atomic<uint32_t> g_enc_width{ZR_ENC_WIDTH_DEFAULT};
 #ifndef ZR_ENC_SPLIT_DEFAULT
 #define ZR_ENC_SPLIT_DEFAULT 0
 #endif
@@ -4255,6 +4264,8 @@ int32_t zr_rans_set_encoder_width(uint32_t lanes) {
     return ZR_OK;
 }
 
+uint32_t zr_rans_get_encoder_width(void) { return g_enc_width.load(std::memory_order_relaxed); }
+
 int32_t zr_rans_set_decoder_ring(int32_t ring) {
     clear_error();
     if (ring < 0 || ring > 2) return set_error(ZR_INVALID_INPUT, "decoder ring must be 0 (auto), 1 or 2");
@@ -4465,11 +4476,9 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
 #else
         auto kenc = w.il ? k_enc_xn<256, 0, true> : k_enc_xn<256, 0, false>;
 #endif
-        // the 1024-lane shape (16 conflict-free table copies, one workgroup per
-        // CU) where whole workgroups of streams fill the buffers: measured in
-        // round 4 at -3 % encoder time but +13 % in the
-        // compaction that follows, so the 256-lane shape stays the default and
-        // zr_rans_set_encoder_width(1024) selects the other
+        // the 512- or 1024-lane shape (8 / 16 table copies, 2 / 1 workgroups per
+        // CU) where whole workgroups of streams fill the buffers (g_enc_width);
+        // the split and fused forms below are the 256-lane shape's
         const uint32_t ew = enc_width();
         const bool wide = ew > 256 && !narrow && a.N % ew == 0;
         if (narrow)
