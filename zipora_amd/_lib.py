@@ -91,6 +91,7 @@ SIGNATURES = [
     ("zr_rans_dtab_from_hist_consume_dev", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp]),
     ("zr_rans_dtab_from_data_dev", ctypes.c_int32, [c_vp, ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp]),
     ("zr_rans_set_encoder_width", ctypes.c_int32, [ctypes.c_uint32]),
+    ("zr_rans_get_encoder_width", ctypes.c_uint32, []),
     ("zr_rans_set_encode_split", ctypes.c_int32, [ctypes.c_int32]),
     ("zr_rans_set_decoder_ring", ctypes.c_int32, [ctypes.c_int32]),
     ("zr_rans_set_encode_fused", ctypes.c_int32, [ctypes.c_int32]),
