@@ -2268,7 +2268,8 @@ constexpr int DT2 = 16;  // steps per tile
 // records written to the workspace scratch area; wide shape only: 64 refills
 // land without their LDS writes, 128 refill loads read a table line instead of
 // the stream, 256 every store of a wave goes to the same 256 B, 512 no wait for
-// the refill loads at the boundaries, 1024 no tile boundaries at all: no refill
+// the refill loads at the boundaries (not launched: faults, see the switch in
+// zr_rans_decode_batch_dev), 1024 no tile boundaries at all: no refill
 // loads, waits, landings or ring checks, i.e. the minimal instruction stream of
 // the chain, the ring reads and the packed stores); the product instantiates ABL = 0.
 //
@@ -4664,8 +4665,9 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
                 case 128: kern = k_dec_xn_fast<1024, 128, ZR_DEC_T8 != 0>; break;
                 case 192: kern = k_dec_xn_fast<1024, 192, ZR_DEC_T8 != 0>; break;
                 case 256: kern = k_dec_xn_fast<1024, 256, ZR_DEC_T8 != 0>; break;
-                case 512: kern = k_dec_xn_fast<1024, 512, ZR_DEC_T8 != 0>; break;
-                case 576: kern = k_dec_xn_fast<1024, 576, ZR_DEC_T8 != 0>; break;
+                // (512 / 576, no wait for the refill loads, are not instantiated: the
+                // loads' destination registers are reused before the data lands, and
+                // in round 5 that ablation faulted the GPU; profiles/r05_dec_abl5.log)
                 case 1024: kern = k_dec_xn_fast<1024, 1024, ZR_DEC_T8 != 0>; break;
                 case 1025: kern = k_dec_xn_fast<1024, 1025, ZR_DEC_T8 != 0>; break;
                 default: break;
