@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Randomised parity sweep of the xN rANS device path against the CPU oracle
+(test infrastructure, run on the GPU box; not part of the pytest suite).
+
+Each case: a random batch geometry (N streams, B buffers, ragged lengths with
+the edge lengths 0, 1, N-1, N, N+1 mixed in), random data kinds per buffer
+(uniform, Zipf, text, one symbol, two symbols, rare symbols), per-buffer or
+shared tables, and an encoder width (256, 512, 1024). The encoded bytes of
+every buffer are compared with the oracle's (rans.rs:338-420 restated) and the
+device decode must return the input. Usage:
+    python3 tools/fuzz_rans.py [seconds] [seed]
+"""
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def data_of(kind, n, rng, zr):
+    if n == 0:
+        return b""
+    if kind == "one":
+        return bytes([rng.randrange(256)]) * n
+    if kind == "two":
+        a, b = rng.randrange(256), rng.randrange(256)
+        return bytes(np.where(np.random.default_rng(rng.randrange(1 << 30)).integers(0, 2, n) == 0, a, b)
+                     .astype(np.uint8))
+    if kind == "rare":
+        d = np.full(n, rng.randrange(256), dtype=np.uint8)
+        k = min(n, 50)
+        pos = np.random.default_rng(rng.randrange(1 << 30)).choice(n, k, replace=False)
+        d[pos] = np.random.default_rng(rng.randrange(1 << 30)).integers(0, 256, k).astype(np.uint8)
+        return d.tobytes()
+    return zr.synth(kind, n, seed=rng.randrange(1 << 62))
+
+
+def main():
+    import torch
+    import oracle_ffi as orc
+    import zipora_amd as zr
+    from zipora_amd.device import RansDeviceBatch
+
+    secs = float(sys.argv[1]) if len(sys.argv) > 1 else 150.0
+    seed = int(sys.argv[2]) if len(sys.argv) > 2 else 12345
+    rng = random.Random(seed)
+    L = zr.load()
+    w0 = L.zr_rans_get_encoder_width()
+    t_end = time.time() + secs
+    cases = bufs = 0
+    try:
+        while time.time() < t_end:
+            N = rng.choice([2, 7, 64, 255, 256, 300, 512, 1000, 1024, 1536, 2048, 4096, 8192])
+            # narrow (B * N <= 2^16) and wide batches
+            B = rng.choice([1, 2, 3, 5]) if rng.random() < 0.3 else max(1, ((1 << 16) // N) + rng.randrange(1, 40))
+            B = min(B, max(1, (24 << 20) // max(1, 40 * N)))
+            base = [0, 1, N - 1, N, N + 1]
+            lens = [base[i] if i < len(base) and rng.random() < 0.5 else
+                    rng.randrange(N, N * rng.choice([2, 8, 40])) for i in range(B)]
+            shared = rng.random() < 0.5
+            width = rng.choice([256, 512, 1024])
+            kinds = [rng.choice(["u", "z", "t", "one", "two", "rare"]) for _ in range(B)]
+            datas = [data_of(k, n, rng, zr) for k, n in zip(kinds, lens)]
+            assert L.zr_rans_set_encoder_width(width) == 0
+            bt = RansDeviceBatch(lens, N, shared_table=shared)
+            raw = bt.new_raw()
+            for b, d in enumerate(datas):
+                if d:
+                    o = bt.raw_off_host[b]
+                    raw[o:o + len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8).to(raw.device)
+            enc = bt.new_enc()
+            bt.full_encode(raw, enc)
+            torch.cuda.synchronize()
+            st = bt.statuses()
+            if shared:
+                tabs = [orc.rans_table(orc.histogram(b"".join(datas)))] * B
+            else:
+                tabs = [orc.rans_table(orc.histogram(d)) for d in datas]
+            for b, d in enumerate(datas):
+                want = orc.rans_encode(tabs[b], N, d)
+                got = bt.encoded(enc, b)
+                if st[b] != 0 or got != want:
+                    raise SystemExit(f"MISMATCH case {cases} seed {seed}: N={N} B={B} shared={shared} "
+                                     f"width={width} buffer {b} len={lens[b]} kind={kinds[b]} status={st[b]} "
+                                     f"got {len(got)} B want {len(want)} B")
+            out = bt.new_raw()
+            bt.decode(enc, out)
+            torch.cuda.synchronize()
+            bt.raise_on_error()
+            for b, d in enumerate(datas):
+                if bt.raw_of(out, b) != d:
+                    raise SystemExit(f"DECODE MISMATCH case {cases}: N={N} B={B} width={width} buffer {b}")
+            cases += 1
+            bufs += B
+            print(f"case {cases}: N={N} B={B} shared={int(shared)} width={width} bytes={sum(lens)} ok",
+                  flush=True)
+    finally:
+        L.zr_rans_set_encoder_width(w0)
+    print(f"fuzz ok: {cases} cases, {bufs} buffers, seed {seed}")
+
+
+if __name__ == "__main__":
+    main()
