@@ -1,0 +1,24 @@
+"""A fixed-seed slice of the randomised rANS parity sweep (tools/fuzz_rans.py):
+random batch geometries (narrow and wide shapes, ragged and edge lengths), data
+kinds, shared or per-buffer tables and encoder widths, every buffer's encoded
+bytes equal to the oracle's (rans.rs:338-420) and decoded back on the device."""
+import importlib.util
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _fuzz():
+    spec = importlib.util.spec_from_file_location("fuzz_rans", os.path.join(ROOT, "tools", "fuzz_rans.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+@pytest.mark.parametrize("seed", [2024, 31337])
+def test_rans_random_batches_match_oracle(zr, oracle, seed):
+    cases, bufs = _fuzz().run(max_cases=40, seed=seed, log=lambda m: None)
+    assert cases == 40 and bufs > 40

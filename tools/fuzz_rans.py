@@ -40,21 +40,21 @@ def data_of(kind, n, rng, zr):
     return zr.synth(kind, n, seed=rng.randrange(1 << 62))
 
 
-def main():
+def run(secs=None, max_cases=None, seed=12345, log=print):
+    """Random cases until secs have passed or max_cases are done; raises
+    AssertionError on the first mismatch. Returns (cases, buffers)."""
     import torch
     import oracle_ffi as orc
     import zipora_amd as zr
     from zipora_amd.device import RansDeviceBatch
 
-    secs = float(sys.argv[1]) if len(sys.argv) > 1 else 150.0
-    seed = int(sys.argv[2]) if len(sys.argv) > 2 else 12345
     rng = random.Random(seed)
     L = zr.load()
     w0 = L.zr_rans_get_encoder_width()
-    t_end = time.time() + secs
+    t_end = time.time() + secs if secs else None
     cases = bufs = 0
     try:
-        while time.time() < t_end:
+        while (t_end is None or time.time() < t_end) and (max_cases is None or cases < max_cases):
             N = rng.choice([2, 7, 64, 255, 256, 300, 512, 1000, 1024, 1536, 2048, 4096, 8192])
             # narrow (B * N <= 2^16) and wide batches
             B = rng.choice([1, 2, 3, 5]) if rng.random() < 0.3 else max(1, ((1 << 16) // N) + rng.randrange(1, 40))
@@ -85,7 +85,7 @@ def main():
                 want = orc.rans_encode(tabs[b], N, d)
                 got = bt.encoded(enc, b)
                 if st[b] != 0 or got != want:
-                    raise SystemExit(f"MISMATCH case {cases} seed {seed}: N={N} B={B} shared={shared} "
+                    raise AssertionError(f"MISMATCH case {cases} seed {seed}: N={N} B={B} shared={shared} "
                                      f"width={width} buffer {b} len={lens[b]} kind={kinds[b]} status={st[b]} "
                                      f"got {len(got)} B want {len(want)} B")
             out = bt.new_raw()
@@ -94,13 +94,19 @@ def main():
             bt.raise_on_error()
             for b, d in enumerate(datas):
                 if bt.raw_of(out, b) != d:
-                    raise SystemExit(f"DECODE MISMATCH case {cases}: N={N} B={B} width={width} buffer {b}")
+                    raise AssertionError(f"DECODE MISMATCH case {cases}: N={N} B={B} width={width} buffer {b}")
             cases += 1
             bufs += B
-            print(f"case {cases}: N={N} B={B} shared={int(shared)} width={width} bytes={sum(lens)} ok",
-                  flush=True)
+            log(f"case {cases}: N={N} B={B} shared={int(shared)} width={width} bytes={sum(lens)} ok")
     finally:
         L.zr_rans_set_encoder_width(w0)
+    return cases, bufs
+
+
+def main():
+    secs = float(sys.argv[1]) if len(sys.argv) > 1 else 150.0
+    seed = int(sys.argv[2]) if len(sys.argv) > 2 else 12345
+    cases, bufs = run(secs=secs, seed=seed, log=lambda m: print(m, flush=True))
     print(f"fuzz ok: {cases} cases, {bufs} buffers, seed {seed}")
 
 
