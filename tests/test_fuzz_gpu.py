@@ -1,4 +1,4 @@
-"""A fixed-seed slice of the randomised rANS parity sweep (tools/fuzz_rans.py):
+"""Fixed-seed slices of the randomised parity sweeps (tools/fuzz_rans.py, tools/fuzz_fse.py):
 random batch geometries (narrow and wide shapes, ragged and edge lengths), data
 kinds, shared or per-buffer tables and encoder widths, every buffer's encoded
 bytes equal to the oracle's (rans.rs:338-420) and decoded back on the device."""
@@ -22,3 +22,16 @@ def _fuzz():
 def test_rans_random_batches_match_oracle(zr, oracle, seed):
     cases, bufs = _fuzz().run(max_cases=40, seed=seed, log=lambda m: None)
     assert cases == 40 and bufs > 40
+
+
+def _fuzz_fse():
+    spec = importlib.util.spec_from_file_location("fuzz_fse", os.path.join(ROOT, "tools", "fuzz_fse.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_fse_random_configs_match_oracle(zr, oracle):
+    """Random FSE data and configs (tools/fuzz_fse.py): bytes equal to the
+    oracle's, decompression error for error with it."""
+    assert _fuzz_fse().run(max_cases=200, seed=99, log=lambda m: None) == 200
