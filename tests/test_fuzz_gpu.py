@@ -1,4 +1,4 @@
-"""Fixed-seed slices of the randomised parity sweeps (tools/fuzz_rans.py, tools/fuzz_fse.py):
+"""Fixed-seed slices of the randomised parity sweeps (tools/fuzz_rans.py, fuzz_fse.py, fuzz_huff.py):
 random batch geometries (narrow and wide shapes, ragged and edge lengths), data
 kinds, shared or per-buffer tables and encoder widths, every buffer's encoded
 bytes equal to the oracle's (rans.rs:338-420) and decoded back on the device."""
@@ -35,3 +35,12 @@ def test_fse_random_configs_match_oracle(zr, oracle):
     """Random FSE data and configs (tools/fuzz_fse.py): bytes equal to the
     oracle's, decompression error for error with it."""
     assert _fuzz_fse().run(max_cases=200, seed=99, log=lambda m: None) == 200
+
+
+def test_huffman_random_inputs_match_oracle(zr, oracle):
+    """Random data through the order-0 and contextual order-1/2 coders
+    (tools/fuzz_huff.py): bytes equal to the oracle's, decoded back."""
+    spec = importlib.util.spec_from_file_location("fuzz_huff", os.path.join(ROOT, "tools", "fuzz_huff.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.run(max_cases=150, seed=7, log=lambda m_: None) == 150
