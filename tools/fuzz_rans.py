@@ -3,7 +3,8 @@
 (test infrastructure, run on the GPU box; not part of the pytest suite).
 
 Each case: a random batch geometry (N streams, B buffers, ragged lengths with
-the edge lengths 0, 1, N-1, N, N+1 mixed in), random data kinds per buffer
+the edge lengths 0, 1, N-1, N, N+1 mixed in; or a record batch, N = 1, up to
+5000 records of 0-4095 bytes at 1/2/4/16-byte aligned offsets), random data kinds per buffer
 (uniform, Zipf, text, one symbol, two symbols, rare symbols), per-buffer or
 shared tables, and an encoder width (256, 512, 1024). The encoded bytes of
 every buffer are compared with the oracle's (rans.rs:338-420 restated) and the
@@ -55,19 +56,29 @@ def run(secs=None, max_cases=None, seed=12345, log=print):
     cases = bufs = 0
     try:
         while (t_end is None or time.time() < t_end) and (max_cases is None or cases < max_cases):
-            N = rng.choice([2, 7, 64, 255, 256, 300, 512, 1000, 1024, 1536, 2048, 4096, 8192])
-            # narrow (B * N <= 2^16) and wide batches
-            B = rng.choice([1, 2, 3, 5]) if rng.random() < 0.3 else max(1, ((1 << 16) // N) + rng.randrange(1, 40))
-            B = min(B, max(1, (24 << 20) // max(1, 40 * N)))
-            base = [0, 1, N - 1, N, N + 1]
-            lens = [base[i] if i < len(base) and rng.random() < 0.5 else
-                    rng.randrange(N, N * rng.choice([2, 8, 40])) for i in range(B)]
+            align = 16
+            if rng.random() < 0.3:
+                # record batches: N = 1 (every buffer one stream, the x1 kernels),
+                # many short records, outputs aligned or not
+                N = 1
+                B = rng.randrange(50, 5000)
+                lens = [rng.choice([0, 1, 7, 8, 15, 16, 31, 32, 63, 64, 127, 128, 129, 1024,
+                                    rng.randrange(0, 4096)]) for _ in range(B)]
+                align = rng.choice([1, 2, 4, 16])
+            else:
+                N = rng.choice([2, 7, 64, 255, 256, 300, 512, 1000, 1024, 1536, 2048, 4096, 8192])
+                # narrow (B * N <= 2^16) and wide batches
+                B = rng.choice([1, 2, 3, 5]) if rng.random() < 0.3 else max(1, ((1 << 16) // N) + rng.randrange(1, 40))
+                B = min(B, max(1, (24 << 20) // max(1, 40 * N)))
+                base = [0, 1, N - 1, N, N + 1]
+                lens = [base[i] if i < len(base) and rng.random() < 0.5 else
+                        rng.randrange(N, N * rng.choice([2, 8, 40])) for i in range(B)]
             shared = rng.random() < 0.5
             width = rng.choice([256, 512, 1024])
             kinds = [rng.choice(["u", "z", "t", "one", "two", "rare"]) for _ in range(B)]
             datas = [data_of(k, n, rng, zr) for k, n in zip(kinds, lens)]
             assert L.zr_rans_set_encoder_width(width) == 0
-            bt = RansDeviceBatch(lens, N, shared_table=shared)
+            bt = RansDeviceBatch(lens, N, shared_table=shared, align=align)
             raw = bt.new_raw()
             for b, d in enumerate(datas):
                 if d:
@@ -97,7 +108,7 @@ def run(secs=None, max_cases=None, seed=12345, log=print):
                     raise AssertionError(f"DECODE MISMATCH case {cases}: N={N} B={B} width={width} buffer {b}")
             cases += 1
             bufs += B
-            log(f"case {cases}: N={N} B={B} shared={int(shared)} width={width} bytes={sum(lens)} ok")
+            log(f"case {cases}: N={N} B={B} shared={int(shared)} width={width} align={align} bytes={sum(lens)} ok")
     finally:
         L.zr_rans_set_encoder_width(w0)
     return cases, bufs
