@@ -2299,7 +2299,10 @@ __device__ __forceinline__ bool arrive_word(uint64_t *word, uint64_t tag, bool &
     uint64_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t nw;
     do {
-        nw = ((old >> 24) == tag ? old + 1 : (tag << 24) | 1) | ((uint64_t)err << 23);
+        // a word of this call holds a count < n (n arrivals complete it, and none
+        // follows): one with this call's tag bits but a count >= n is stale
+        // workspace content (round 5's corrupted-input sweep met one) and restarts
+        nw = ((old >> 24) == tag && (old & 0x7FFFFF) < n ? old + 1 : (tag << 24) | 1) | ((uint64_t)err << 23);
     } while (!__hip_atomic_compare_exchange_weak(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT));
     err = (nw >> 23) & 1;  // the errors of every arrival so far
