@@ -1,4 +1,4 @@
-"""Fixed-seed slices of the randomised parity sweeps (tools/fuzz_rans.py, fuzz_fse.py, fuzz_huff.py):
+"""Fixed-seed slices of the randomised parity sweeps (tools/fuzz_rans.py, fuzz_fse.py, fuzz_huff.py, fuzz_rans_corrupt.py):
 random batch geometries (narrow and wide shapes, ragged and edge lengths), data
 kinds, shared or per-buffer tables and encoder widths, every buffer's encoded
 bytes equal to the oracle's (rans.rs:338-420) and decoded back on the device."""
@@ -44,3 +44,15 @@ def test_huffman_random_inputs_match_oracle(zr, oracle):
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     assert m.run(max_cases=150, seed=7, log=lambda m_: None) == 150
+
+
+def test_rans_corrupted_batches_match_oracle(zr, oracle):
+    """Corrupted encodings (tools/fuzz_rans_corrupt.py: states, lengths, random
+    bytes, enc_len) decoded over a garbage-filled status array: error for error
+    and byte for byte with the oracle."""
+    spec = importlib.util.spec_from_file_location("fuzz_rans_corrupt",
+                                                  os.path.join(ROOT, "tools", "fuzz_rans_corrupt.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    cases, bad = m.run(max_cases=40, seed=707, log=lambda m_: None)
+    assert cases == 40 and bad > 0
