@@ -49,18 +49,6 @@ def parse():
     p.add_argument("--pipeline", action="store_true",
                    help="rans: two distinct batches alternate; each step codes one (encode -> decode on the "
                         "main stream) while the histogram + table of the next one run on a second stream")
-    p.add_argument("--enc-width", type=int, default=0, choices=[0, 256, 512, 1024],
-                   help="rans: the xN encoder's workgroup width (zr_rans_set_encoder_width; 0: the library's default)")
-    p.add_argument("--dec-ring", type=int, default=0, choices=[0, 1, 2],
-                   help="rans: the xN decoder's ring (zr_rans_set_decoder_ring): 0 auto, 1 VGPR-staged "
-                        "(k_dec_xn_fast), 2 LDS-DMA chunks (k_dec_xn_dma, 8 waves per SIMD)")
-    p.add_argument("--enc-fused", type=int, default=None, choices=[0, 1],
-                   help="rans: encode + compaction in one launch with look-back (zr_rans_set_encode_fused; "
-                        "default: the library's)")
-    p.add_argument("--enc-split", type=int, default=None, choices=[0, 1, 2, 3],
-                   help="rans: encode a wide batch in two parts (the first q/4 of the buffers, then the rest), "
-                        "the second part's encoder and the first part's compaction in one dispatch "
-                        "(zr_rans_set_encode_split; default: the library's)")
     p.add_argument("--records", type=int, default=1 << 20)
     p.add_argument("--fse-block-kib", type=int, default=64)
     p.add_argument("--dry-run", action="store_true",
@@ -305,7 +293,7 @@ def run_fse(args, torch, dist, world, rank, dev, zr, L):
 
 
 RANS_SYMS = {"rans_encode": "k_enc_xn", "rans_decode": "k_dec_xn_fast", "rans_compact": "k_enc_compact_lds",
-             "histogram": "k_hist", "rans_encode_compact": "k_enc_cmp_fused"}
+             "histogram": "k_hist"}
 KMS_SOURCE = ("instrumented passes before the timed region (8 steps per kernel, that kernel alone HIP-event "
               "timed on every 4th step); the roofline's avg_launch_ms is the dominant kernel's, timed alone on "
               "every 4th step of the timed region")
@@ -809,14 +797,8 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
             raise SystemExit("decode mismatch after the first step")
 
     dt, dom, dom_ms, kms, tms = _measure(torch, dist, world, dev, L, step, args,
-                                         ["rans_encode", "rans_encode_compact", "rans_decode", "rans_compact",
-                                          "histogram"],
+                                         ["rans_encode", "rans_decode", "rans_compact", "histogram"],
                                          also=["rans_decode"])
-    # split encode (zr_rans_set_encode_split): rans_encode is the lower half's
-    # encoder, rans_encode_compact the upper half's encoder with the lower half's
-    # compaction, rans_compact the upper half's compaction
-    split = kms.get("rans_encode_compact", 0) > 0
-
     if not diag:
         b_, r_ = last_raw()
         b_.raise_on_error()
@@ -850,22 +832,8 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
     syms = dict(RANS_SYMS)  # the decode kernel this batch ran (zr_rans_decoder_kernel)
     if hasattr(L, "zr_rans_decoder_kernel"):
         syms["rans_decode"] = L.zr_rans_decoder_kernel(B, N).decode()
-    # encode + compaction in one launch (k_enc_lb): no separate compaction ran; its
-    # roofline counts the encode's algorithmic bytes (N_in + C) over the fused time
-    fused = (hasattr(L, "zr_rans_get_encode_fused") and L.zr_rans_get_encode_fused() == 1
-             and kms.get("rans_compact", 0) == 0 and not split)
-    if fused:
-        syms["rans_encode"] = "k_enc_lb"
     rans_bytes = {"rans_encode": total + comp_bytes, "rans_decode": comp_bytes + total,
                   "rans_compact": 2 * comp_bytes, "histogram": total}
-    if split:
-        q = args.enc_split if args.enc_split is not None else int(L.zr_rans_get_encode_split())
-        h = (B * q + 2) // 4
-        lens = [int(v) for v in bt.enc_len.tolist()]
-        c_lo, c_hi = sum(lens[:h]), sum(lens[h:])
-        r_lo, r_hi = h * n, (B - h) * n
-        rans_bytes.update({"rans_encode": r_lo + c_lo, "rans_encode_compact": r_hi + c_hi + 2 * c_lo,
-                           "rans_compact": 2 * c_hi})
 
     res = {
         "metric": "GiB/s encode+decode (device-resident), rANS O0, 256 MiB, 1/2/4/8 MI355X",
@@ -891,14 +859,7 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
                                 f"{B} x {n >> 20} MiB buffers, {N}-way interleaved streams each "
                                 f"({B * N} streams), shared table (histogram all-reduce over ranks)"),
                    "buffers": B, "buffer_bytes": n, "n_streams": N, "parallelism": f"shard{world}",
-                   "encoder_lanes": (64 if B * N <= 1 << 16 else ew if N % (ew := int(L.zr_rans_get_encoder_width())) == 0
-                                     else 256),
-                   **({"encode_schedule": f"split at buffer {h}: encoder(0..{h}) -> encoder({h}..{B}) + "
-                                          f"compaction(0..{h}) in one dispatch -> compaction({h}..{B})"}
-                      if split else {}),
-                   **({"encode_schedule": "encode + compaction in one launch (k_enc_lb: each encoder workgroup "
-                                          "compacts its own streams after a look-back on its buffer's block sums)"}
-                      if fused else {}),
+                   "encoder_lanes": 64 if B * N <= 1 << 16 else 256,
                    **({"pipelined": "two distinct 256 MiB batches alternate; step k codes one batch (encode -> "
                                     "decode) while the histogram + table of the other run on a second HIP stream"}
                       if pipe else {})},
@@ -1084,16 +1045,6 @@ def main():
     import zipora_amd as zr
     L = zr.load()
     L.zr_set_device(local)
-    # the split and fused encodes are forms of the 256-lane encoder shape
-    ew = args.enc_width or (256 if args.enc_fused or args.enc_split else 0)
-    if ew and L.zr_rans_set_encoder_width(ew):
-        raise SystemExit(f"encoder width {ew} refused")
-    if args.dec_ring and L.zr_rans_set_decoder_ring(args.dec_ring):
-        raise SystemExit(f"decoder ring {args.dec_ring} refused")
-    if args.enc_fused is not None and L.zr_rans_set_encode_fused(args.enc_fused):
-        raise SystemExit(f"encode fused {args.enc_fused} refused")
-    if args.enc_split is not None and L.zr_rans_set_encode_split(args.enc_split):
-        raise SystemExit(f"encode split {args.enc_split} refused")
 
     copy_ceiling(torch, dev, L)
     if args.workload in ("fse", "o1", "blob"):

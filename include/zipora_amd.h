@@ -26,8 +26,7 @@
  * per-buffer status into a device int32 array; read it after synchronising.
  * Graph capture: zr_rans_encode/decode_batch_dev, zr_histogram_dev,
  * zr_rans_dtab_from_hist*_dev and the RCCL calls may be captured into a HIP
- * graph and replayed (zr_rans_decode_batch_dev then takes its capture-safe
- * path: no host-side call counter). Every other _dev call returns
+ * graph and replayed (they keep no host-side state). Every other _dev call returns
  * ZR_UNSUPPORTED on a capturing stream: zr_rans_dtab_upload and
  * zr_huff_decode_dev stage host data through memory a host callback frees,
  * zr_rans_dtab_from_data_dev picks its ticket counters by a host counter, and
@@ -169,55 +168,26 @@ int32_t zr_rans_dtab_from_hist_consume_dev(uint32_t *hist_dev, uint32_t n_tables
  * slot, and a table would then be built before its histogram is complete). */
 int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *batch, uint32_t *hist_dev,
                                    void *dtab_dev, void *stream);
-/* Tuning (no reference counterpart): the xN decoder's ring for batches of more
- * than 2^16 streams, process-wide. 0 (default) and 1: the VGPR-staged ring
- * decoder (one 1024-lane workgroup per CU, 4 waves per SIMD); 2: the LDS-DMA
- * ring decoder (two 1024-lane workgroups per CU, 8 waves per SIMD, N >= 64),
- * measured slower. Both decode the same format
- * bit for bit (rans.rs:555-651). */
-int32_t zr_rans_set_decoder_ring(int32_t ring);
-/* Tuning (no reference counterpart): encode and stream compaction in one
- * launch, process-wide (1 on, 0 off): every 256-stream encoder workgroup
- * compacts its own streams after a look-back on the byte sums of its buffer's
- * lower blocks (the same reference layout, rans.rs:402-419). Applies to
- * batches of > 2^16 streams of short streams (<= 64 blocks of 256 streams per
- * buffer, <= ~1.2 KiB of output per stream), not under graph capture. */
-int32_t zr_rans_set_encode_fused(int32_t on);
-int32_t zr_rans_get_encode_fused(void);
-/* Tuning (no reference counterpart): the stream compaction of an xN encode
- * (batches of short streams, <= 64 blocks of 256 streams per buffer) as a
- * software pipeline of wg_per_cu (1..8) workgroups per CU walking the 16-stream
- * groups, 0 (the default) one workgroup per group; the same bytes
- * (rans.rs:402-419). Measured slower. */
-int32_t zr_rans_set_compact_pipe(int32_t wg_per_cu);
 /* The name of the xN decode kernel a batch of n_buffers x n_streams (every
- * buffer at least n_streams bytes) runs under the current setting (reports and
- * profiles; a static string). */
+ * buffer at least n_streams bytes) runs (reports and profiles; a static
+ * string). No codec setting is process-wide: a call's kernels depend only on
+ * its batch geometry. */
 const char *zr_rans_decoder_kernel(uint32_t n_buffers, uint32_t n_streams);
-/* Tuning (no reference counterpart): the workgroup width of the xN encoder for
- * batches of more than 2^16 streams, process-wide: 256 (default; 4 copies of
- * the encode table, 4 workgroups per CU), 512 (8 copies, 2 per CU) or 1024 (one
- * workgroup per CU with 16 conflict-free copies); 512 and 1024 are used where
- * n_streams is a multiple of the width, 256 otherwise. The split and fused
- * encodes (below) apply to the 256-lane shape. Output bytes are identical. */
-int32_t zr_rans_set_encoder_width(uint32_t lanes);
-/* the current setting of zr_rans_set_encoder_width */
-uint32_t zr_rans_get_encoder_width(void);
-/* Tuning (no reference counterpart), process-wide: q = 1..3 codes the xN encode
- * of a batch of at least 2^18 streams (256-lane encoder) as the encoder of the
- * first round(B * q / 4) buffers, then the other buffers' encoder and the first
- * part's compaction in one dispatch, then the other part's compaction; 0 runs
- * encoder then compaction over the whole batch. Output bytes are identical. */
-int32_t zr_rans_set_encode_split(int32_t quarters);
-/* the current setting of zr_rans_set_encode_split */
-int32_t zr_rans_get_encode_split(void);
-/* bytes of device workspace needed by encode/decode of this batch geometry */
+/* bytes of device workspace needed by encode/decode of this batch geometry.
+ * Workspace contract: scratch owned by one call at a time (calls that share a
+ * workspace must be ordered, e.g. on one stream); its content before a call
+ * is never read as input, so it needs no initialisation and any content
+ * (garbage, another geometry's arrays) gives the same results and statuses. */
 size_t zr_rans_workspace_bytes(uint32_t n_buffers, uint32_t n_streams, uint64_t max_len);
 /* batched Rans64Encoder::encode: raw -> enc (enc + enc_off[b] must hold
  * zr_rans_encode_bound(len[b], n_streams) bytes) */
 int32_t zr_rans_encode_batch_dev(const zr_rans_batch *batch, const uint8_t *raw, uint8_t *enc,
                                  void *workspace, size_t workspace_bytes, void *stream);
-/* batched Rans64Decoder::decode: enc -> raw */
+/* batched Rans64Decoder::decode: enc -> raw. status[b] is set for every
+ * buffer: the call first clears the statuses to ZR_OK (stream-ordered, 4 B per
+ * buffer) and its kernels store ZR_INVALID_INPUT for a buffer whose header,
+ * stream lengths or renormalisation reads are invalid (rans.rs:480-482,
+ * :563-568, :601-610). */
 int32_t zr_rans_decode_batch_dev(const zr_rans_batch *batch, const uint8_t *enc, uint8_t *raw,
                                  void *workspace, size_t workspace_bytes, void *stream);
 

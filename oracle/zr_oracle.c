@@ -654,13 +654,14 @@ int or_fse_compress_freqs(const or_fse_config *c, const uint32_t *freqs, const u
    state never drops below 1. (The reference's `pos + 4 <= len` guard always
    holds once pos >= 4, so the word is always read.) Returns the new state. */
 uint64_t or_fse_renormalize_decode(uint64_t x, const uint8_t *in, size_t len, size_t *pos) {
-    (void)len;
     if (x < 65536 && *pos > 0) {
         if (*pos >= 4) {
             *pos -= 4;
-            x = (x << 32) | rd_u32(in + *pos);
+            x <<= 32;
+            if (*pos + 4 <= len) x |= rd_u32(in + *pos); /* fse.rs:722-726: no word read past the input */
         } else {
             *pos -= 1;
+            if (*pos >= len) return 0; /* input[*pos] out of bounds: the reference panics (fse.rs:729) */
             x = (x << 8) | in[*pos];
         }
     }

@@ -73,7 +73,9 @@ int or_fse_decompress(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
 int or_fse_decompressed_size(const uint8_t *in, size_t n, size_t *out_len);
 /* The portable mul_hi of fse.rs:618-628 (wrapping middle sum). */
 uint64_t or_fse_mul_hi(uint64_t a, uint64_t b);
-/* FseTable::renormalize_decode, fse.rs:704-735 (pos moves down; returns the state) */
+/* FseTable::renormalize_decode, fse.rs:704-735 (pos moves down; returns the state;
+ * a word position past len shifts without a read, as fse.rs:722; returns 0
+ * where the reference's one-byte read would index past the input and panic) */
 uint64_t or_fse_renormalize_decode(uint64_t x, const uint8_t *in, size_t len, size_t *pos);
 
 /* ---- Huffman O0 (src/entropy/huffman/{tree,encoder,decoder}.rs) ---- */

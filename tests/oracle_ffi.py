@@ -231,6 +231,8 @@ def fse_renormalize_decode(state, data, pos):
     p = sz(pos)
     b, n = _buf(data)
     x = lib().or_fse_renormalize_decode(state, b, n, ctypes.byref(p))
+    if x == 0:  # input[*pos] past the input: a panic in the reference (fse.rs:729)
+        raise OracleError("renormalize_decode: index out of bounds")
     return x, p.value
 
 

@@ -125,29 +125,15 @@ def test_single_buffer_many_streams(zr, oracle, N):
     assert fb == 0, f"{fb} of {N} streams fell back"
 
 
-@pytest.fixture
-def dec_ring(zr):
-    """Sets the xN decoder's ring for one test (zr_rans_set_decoder_ring), auto again after it."""
-    L = zr.load()
-
-    def set_r(r):
-        assert L.zr_rans_set_decoder_ring(r) == 0
-
-    yield set_r
-    L.zr_rans_set_decoder_ring(0)
-
-
 @pytest.mark.parametrize("lens,N,kind,check", [
-    ([4 << 20] * 64, 4096, "u", 2),          # the headline shape on the DMA ring (2^18 lanes)
     ([4 << 20] * 16, 4096, "z", 2),
-    ([4 << 20] * 16, 4096, "t", 2),
-    ([(4 << 20) + 4096 * 17 + 5] * 20, 4096, "u", 2),   # ragged rows (tail with chunks in flight)
-    ([256 << 20], 1 << 19, "u", 1),          # one buffer, N = 2^19
+    ([(4 << 20) + 4096 * 17 + 5] * 20, 4096, "u", 2),   # ragged rows (tail with refills in flight)
+    ([256 << 20], 1 << 19, "u", 1),          # one buffer, N = 2^19 (two rounds of workgroups)
     ([3_000_001, 1_000_003, 77_777], 1 << 16, "t", 3),  # ragged buffers (the last one x1), 3 x 2^16 lanes
 ])
-def test_dma_ring_decoder(zr, oracle, dec_ring, lens, N, kind, check):
-    """k_dec_xn_dma (the LDS-DMA chunk ring, 8 waves per SIMD) forced on: the
-    same bytes as the oracle's encode and the input back, no generic lanes."""
-    dec_ring(2)
+def test_wide_decoder_shapes(zr, oracle, lens, N, kind, check):
+    """k_dec_xn_fast on the shapes round 5 ran through its LDS-DMA variant (now
+    removed): the same bytes as the oracle's encode and the input back, no
+    generic lanes."""
     fb = _batch_roundtrip(zr, oracle, lens, N, kind, 0xD3A + N, check_bufs=check)
     assert fb == 0, f"{fb} streams fell back"

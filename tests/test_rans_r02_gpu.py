@@ -17,19 +17,6 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.fixture
-def enc_width(zr):
-    """Sets the xN encoder's workgroup width for one test, 256 again after it."""
-    L = zr.load()
-
-    def set_w(n):
-        assert L.zr_rans_set_encoder_width(n) == 0
-
-    was = L.zr_rans_get_encoder_width()
-    yield set_w
-    L.zr_rans_set_encoder_width(was)
-
-
 def _fill(bt, datas):
     import torch
     raw = bt.new_raw()
@@ -68,17 +55,13 @@ def test_rans_literal_config_full_size(zr, oracle):
     assert torch.equal(out[:n], raw)
 
 
-@pytest.mark.parametrize("N,B,width", [(4096, 24, 256), (1000, 70, 256), (4096, 24, 1024), (1024, 70, 1024),
-                                       (2048, 40, 1024), (8192, 10, 1024), (4096, 24, 512), (512, 140, 512),
-                                       (1536, 50, 512), (1000, 70, 512)])
-def test_rans_wide_shape_ragged(zr, oracle, N, B, width, enc_width):
-    """More than 2^16 streams in the batch: 256-lane encoder workgroups, or
-    (zr_rans_set_encoder_width(512 / 1024), N a multiple of the width; else the
-    256-lane ones) the 512-lane ones with 8 table copies and the 1024-lane ones
-    with 16, 1024-lane decoder workgroups, with ragged, tiny (x1 layout) and
-    empty buffers mixed in."""
+@pytest.mark.parametrize("N,B", [(4096, 24), (1000, 70), (1024, 70), (2048, 40), (8192, 10), (512, 140),
+                                 (1536, 50)])
+def test_rans_wide_shape_ragged(zr, oracle, N, B):
+    """More than 2^16 streams in the batch: 256-lane encoder workgroups and
+    1024-lane decoder workgroups, with ragged, tiny (x1 layout) and empty
+    buffers mixed in."""
     import torch
-    enc_width(width)
     from zipora_amd.device import RansDeviceBatch
     rnd = random.Random(N)
     base = [0, 1, N - 1, N, N + 1, 50000, 123457, 1 << 18, 3 * N + 7]
@@ -130,16 +113,13 @@ def test_rans_narrow_shape_ragged(zr, oracle, N):
 @pytest.mark.parametrize("N,per,B,skew", [(100, 1208, 3, False), (100, 1209, 3, False), (100, 1208, 2, True),
                                            (4096, 1208, 17, False), (4096, 1208, 17, True), (1000, 300, 70, True),
                                            (4096, 1209, 17, True)])
-@pytest.mark.parametrize("width", [256, 512, 1024])
-def test_rans_scratch_layouts(zr, oracle, N, per, B, skew, width, enc_width):
+def test_rans_scratch_layouts(zr, oracle, N, per, B, skew):
     """Both scratch layouts of the xN encoder (RansWork::il): per-stream capacity
     2 * per + 16 = 2432 B is the largest lane-interleaved one, 2434 B the
     smallest stream-contiguous one. Groups of 16 streams whose destination spans
     two compaction windows, and (skew) streams of very different lengths in one
-    group: every third stream of the period-N interleave sees one constant byte.
-    width 512 / 1024: the same with the 512- or 1024-lane encoder where N allows."""
+    group: every third stream of the period-N interleave sees one constant byte."""
     import torch
-    enc_width(width)
     from zipora_amd.device import RansDeviceBatch
     lens = [N * per - (b % 3) for b in range(B)]
     datas = []

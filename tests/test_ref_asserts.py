@@ -292,6 +292,14 @@ def test_fse_renormalize_decode_single_byte_steps(oracle):
     assert oracle.fse_renormalize_decode(100, bytes([7]), 0) == (100, 0)
     assert oracle.fse_renormalize_decode(1 << 16, bytes([7, 8]), 2) == (1 << 16, 2)
     assert oracle.fse_renormalize_decode(0, b"", 0) == (1, 0)
+    # pos past the input: a word position beyond len shifts the state
+    # and reads nothing (fse.rs:722-726's `*pos + BLOCK_SIZE <= input.len()`);
+    # a one-byte read past it indexes out of bounds, which panics in the reference
+    assert oracle.fse_renormalize_decode(100, bytes([1, 2, 3]), 9) == (100 << 32, 5)
+    x, pos = oracle.fse_renormalize_decode(100, bytes([1, 2, 3, 4, 5, 6]), 7)
+    assert (x, pos) == ((100 << 32), 3)
+    with pytest.raises(oracle.OracleError):
+        oracle.fse_renormalize_decode(100, bytes([1]), 3)
 
 
 def _f5_with_word_area(words, state, orig_len, nsym=256):

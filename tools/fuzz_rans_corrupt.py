@@ -5,8 +5,12 @@ batch (tools/fuzz_rans.py geometries, narrow / wide / record batches), then
 corrupts about half of its buffers (a state set to a random 64-bit value, a
 stream length moved or raised, random bytes overwritten anywhere in the
 buffer, enc_len cut short or raised) and decodes on the device over a
-garbage-filled status array. Every buffer must match the oracle
-(rans.rs:449-651 restated) error for error and byte for byte.
+garbage-filled status array and a workspace filled with one of four patterns
+(random bytes, all ones, zeros, or round 5's epoch-tagged arrival words: tag
+<< 24 | error << 23 | count with the tags round 5's call counter gave a fresh
+process and counts below the arrivals a buffer needs; ws_fill). Every buffer
+must match the oracle (rans.rs:449-651 restated) error for error and byte for
+byte.
 Usage: python3 tools/fuzz_rans_corrupt.py [seconds] [seed]
 """
 import os
@@ -18,6 +22,32 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def ws_fill(ws, rng, kind, n_arrivals=8):
+    """Fills a workspace tensor (uint8, device) with pattern `kind`: 0 random
+    bytes, 1 0xFF, 2 zeros, 3 round 5's arrival words (the decoder no longer
+    reads any of it; the patterns check that no status depends on it)."""
+    import numpy as np
+    import torch
+    n = ws.numel()
+    if kind == 0:
+        h = np.random.default_rng(rng.randrange(1 << 30)).integers(0, 256, n, dtype=np.uint8)
+    elif kind == 1:
+        h = np.full(n, 0xFF, dtype=np.uint8)
+    elif kind == 2:
+        h = np.zeros(n, dtype=np.uint8)
+    else:
+        nw = n // 8
+        k = np.arange(nw, dtype=np.uint64)
+        # the tags of a fresh process's first 64 calls under round 5's counter
+        tag = (np.uint64(0x9E3779B97F4A7C15) + np.uint64(1) + (k % np.uint64(64))) & np.uint64((1 << 40) - 1)
+        cnt = k % np.uint64(max(1, n_arrivals))
+        err = (k // np.uint64(3)) & np.uint64(1)
+        words = (tag << np.uint64(24)) | (err << np.uint64(23)) | cnt
+        h = np.zeros(n, dtype=np.uint8)
+        h[:nw * 8] = words.view(np.uint8)
+    ws.copy_(torch.from_numpy(h).to(ws.device))
 
 
 def run(secs=None, max_cases=None, seed=12345, log=print):
@@ -90,14 +120,8 @@ def run(secs=None, max_cases=None, seed=12345, log=print):
         enc.copy_(torch.frombuffer(host, dtype=torch.uint8).to(enc.device))
         bt.enc_len.copy_(torch.tensor(enc_len, dtype=torch.int64))
         bt.status.fill_(-3)
-        if os.environ.get("FUZZ_ZERO_WS"):  # diagnostic: the decode over a zeroed workspace
-            bt.ws.zero_()
-        # diagnostic: the arrival words (RansWork::blockoff) before the decode
-        ru = lambda x: (x + 255) // 256 * 256
-        base = ru(bt.ws.data_ptr()) - bt.ws.data_ptr()
-        nblk = (N + 255) // 256
-        bo = base + 3 * ru(B * N * 4) + ru(B * nblk * 8)
-        words = bt.ws[bo:bo + B * nblk * 8].cpu().numpy().view("<u8").tolist()
+        fill = rng.randrange(4)
+        ws_fill(bt.ws, rng, fill)
         out = bt.new_raw()
         bt.decode(enc, out)
         torch.cuda.synchronize()
@@ -117,13 +141,11 @@ def run(secs=None, max_cases=None, seed=12345, log=print):
                            "orig": orig[o:o + max(enc_len0[b], enc_len[b])].hex(),
                            "corrupted": bytes(host[o:o + max(enc_len0[b], enc_len[b])]).hex(),
                            "data": datas[b].hex(), "status": st[b],
-                           "decoded": bt.raw_of(out, b).hex(),
-                           "arrival_word_before": hex(words[b * nblk]) if b * nblk < len(words) else None,
-                           "arrival_words_around": [hex(x) for x in words[max(0, b * nblk - 2):b * nblk + 3]]},
+                           "decoded": bt.raw_of(out, b).hex(), "ws_fill": fill},
                           open(dump, "w"))
                 raise AssertionError(f"MISMATCH case {cases} seed {seed}: N={N} B={B} buffer {b} "
                                      f"len={lens[b]} status={st[b]} oracle={'err' if ref is None else 'ok'} "
-                                     f"corruption: {what[b] or 'none'}; enc_len {enc_len[b]}; "
+                                     f"corruption: {what[b] or 'none'}; enc_len {enc_len[b]}; workspace fill {fill}; "
                                      f"neighbours {what[max(0, b - 2):b + 3]}")
         cases += 1
         log(f"case {cases}: N={N} B={B} corrupted so far {bad_bufs} ok")

@@ -90,15 +90,7 @@ SIGNATURES = [
     ("zr_rans_dtab_from_hist_dev", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp]),
     ("zr_rans_dtab_from_hist_consume_dev", ctypes.c_int32, [c_vp, ctypes.c_uint32, c_vp, c_vp]),
     ("zr_rans_dtab_from_data_dev", ctypes.c_int32, [c_vp, ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp]),
-    ("zr_rans_set_encoder_width", ctypes.c_int32, [ctypes.c_uint32]),
-    ("zr_rans_get_encoder_width", ctypes.c_uint32, []),
-    ("zr_rans_set_encode_split", ctypes.c_int32, [ctypes.c_int32]),
-    ("zr_rans_set_decoder_ring", ctypes.c_int32, [ctypes.c_int32]),
-    ("zr_rans_set_encode_fused", ctypes.c_int32, [ctypes.c_int32]),
-    ("zr_rans_get_encode_fused", ctypes.c_int32, []),
-    ("zr_rans_set_compact_pipe", ctypes.c_int32, [ctypes.c_int32]),
     ("zr_rans_decoder_kernel", ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint32]),
-    ("zr_rans_get_encode_split", ctypes.c_int32, []),
     ("zr_rans_workspace_bytes", c_sz, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     ("zr_rans_encode_batch_dev", ctypes.c_int32, [ctypes.POINTER(RansBatch), c_vp, c_vp, c_vp, c_sz,
                                                   c_vp]),

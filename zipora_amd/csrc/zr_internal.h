@@ -76,9 +76,12 @@ __host__ __device__ inline uint32_t enc_rcp(uint32_t f) {
     return f ? (uint32_t)(((1ull << (24 + enc_rsh(f))) + f - 1) / f) : 0u;
 }
 // enc_rcp without a 64-bit division (device table builds)
-// floor(num / d) for num < 2^53, d >= 1: the f64 reciprocal (v_rcp_f64 and one
-// Newton step) gives a quotient within one of the floor either way, corrected
-// by the remainder's sign and size (no IEEE division sequence on the chain)
+// floor(num / d) for d >= 1 and num < 2^50: the f64 reciprocal (v_rcp_f64 and
+// one Newton step, relative error ~2^-51) and the product's rounding put
+// trunc(num * r) within one of the floor while num / d < 2^50, and the
+// remainder's sign and size correct it by one (no IEEE division sequence on
+// the chain). Beyond that bound the error can exceed one: not exact. Callers
+// stay far below it (the table build: num < 2^44; enc_rcp_fast: num < 2^37).
 __device__ inline uint64_t floor_div_u64(uint64_t num, uint32_t d) {
     const double dd = (double)d;
     double r = __builtin_amdgcn_rcp(dd);
