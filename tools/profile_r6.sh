@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-5 profile (round 4's, plus the one-buffer N = 2^18 shape): kernel-trace stats of every bench workload, PMC traffic
+# Round-6 profile (round 5 recipe): kernel-trace stats of every bench workload, PMC traffic
 # (FETCH_SIZE and WRITE_SIZE in separate passes), SQ counters, and the default
 # bench command under a kernel trace (its JSON line + the timed region).
 set -o pipefail
-R=${1:-r05}
+R=${1:-r06}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/prof_$R
 mkdir -p $O/summary
