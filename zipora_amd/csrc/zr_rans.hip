@@ -1011,9 +1011,12 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     const bool body_ok = vec_in && (uint64_t)(blk + 1) * EW <= N && (uint64_t)ETILE * N < (1ull << 32);
     const uint32_t loff = lr * N + col;
     const bool wave_all = (uint64_t)blk * EW + (tid & ~63u) + 64 <= N;  // wave-uniform
-    // tiles t < tfast have every row below cmax - 1 (t * ETILE + ETILE < cmax):
-    // a 32-bit scalar compare per tile instead of two 64-bit ones
-    const uint32_t tfast = (uint32_t)min((cmax - 1) / ETILE, (uint64_t)0xFFFFFFFFu);
+    // tiles t < tfast have every row below floor(n / N), the symbol count every
+    // stream has ((t + 1) * ETILE <= n / N), so all 2^18 streams of a buffer
+    // whose length N divides code every tile in the fast form (the bound was
+    // cmax - 1 before: the top tile took the general form): a 32-bit scalar
+    // compare per tile instead of two 64-bit ones
+    const uint32_t tfast = (uint32_t)min((n / N) / ETILE, (uint64_t)0xFFFFFFFFu);
     // A one-wave workgroup (EW = 64) needs no barrier: a wave's LDS accesses
     // complete in program order (the fences pin the compiler). Wider
     // workgroups keep the shared tile: wave-private 64-column tiles split each
