@@ -109,3 +109,65 @@ def test_decode_status_independent_of_workspace(zr, oracle, N, B, per, fill):
                     assert bt.raw_of(out, b) == ref, f"buffer {b}"
             if not corrupt:
                 assert all(s == 0 for s in st)
+
+
+@pytest.mark.parametrize("fill", [3, 1, 0])
+def test_x1_and_mixed_status_independent_of_workspace(zr, oracle, fill):
+    """The x1 decoders over an adversarial workspace: k_dec_x1_fast leaves a
+    taken flag per record in the workspace for k_dec_x1_ring, written for every
+    record in the same call. A record batch (N = 1: 3000 records of 0-2000 B,
+    some corrupted: a raised state, a cut record) and a mixed batch (N = 4096,
+    buffers shorter than N take the x1 layout beside xN ones), each decoded
+    twice on one workspace: statuses and bytes equal the oracle's
+    (rans.rs:510-552 decode_single, :555-651)."""
+    import torch
+    from fuzz_rans_corrupt import ws_fill
+    from zipora_amd.device import RansDeviceBatch
+    rng = random.Random(77 + fill)
+    for N, lens in ((1, [rng.choice([0, 1, 15, 16, 17, 1024, rng.randrange(0, 2000)]) for _ in range(3000)]),
+                    (4096, [4096 * 20 + 3, 100, 0, 4095, 4096 * 33, 1, 5000, 4096 * 7 + 11] * 3)):
+        datas = [zr.synth("tu"[b % 2], n, seed=500 + b) if n else b"" for b, n in enumerate(lens)]
+        B = len(lens)
+        bt = RansDeviceBatch(lens, N, shared_table=True)
+        raw = bt.new_raw()
+        for b, d in enumerate(datas):
+            if d:
+                o = bt.raw_off_host[b]
+                raw[o:o + len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+        enc = bt.new_enc()
+        bt.full_encode(raw, enc)
+        torch.cuda.synchronize()
+        bt.raise_on_error()
+        tab = oracle.rans_table(oracle.histogram(b"".join(datas)))
+        host = bytearray(enc.cpu().numpy().tobytes())
+        enc_len = bt.enc_len.cpu().tolist()
+        for b in range(0, B, 7):  # corrupt every 7th non-empty buffer
+            o, L = bt.enc_off_host[b], enc_len[b]
+            if L < 9:
+                continue
+            if (b // 7) % 2:
+                s = (L - 8) if (N <= 1 or lens[b] < N) else 8 * rng.randrange(N)
+                host[o + s + 7] |= 0x80  # a state far out of range
+            else:
+                enc_len[b] = L - 1 - rng.randrange(min(L - 1, 6))  # cut short
+        e2 = torch.frombuffer(host, dtype=torch.uint8).cuda()
+        bt.enc_len.copy_(torch.tensor(enc_len, dtype=torch.int64))
+        for rep in range(2):
+            if rep == 0:
+                ws_fill(bt.ws, rng, fill, n_arrivals=8)
+            bt.status.fill_(-3)
+            out = bt.new_raw()
+            bt.decode(e2, out)
+            torch.cuda.synchronize()
+            st = bt.statuses()
+            for b in range(B):
+                o = bt.enc_off_host[b]
+                try:
+                    ref = oracle.rans_decode(tab, N, bytes(host[o:o + enc_len[b]]), lens[b])
+                except oracle.OracleError:
+                    ref = None
+                if ref is None:
+                    assert st[b] == zr._lib.ZR_INVALID_INPUT, f"N={N} buffer {b}: status {st[b]}, oracle error"
+                else:
+                    assert st[b] == 0, f"N={N} buffer {b}: status {st[b]}, oracle ok"
+                    assert bt.raw_of(out, b) == ref, f"N={N} buffer {b}"
