@@ -592,16 +592,34 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n, v4u &reg) {
 // 2: conflict-free table reads); the product instantiates ABL = 0.
 //
 // LDS (one array, carved by hand so that the output ring sits at offset 0 and
-// a ring address wraps with one AND): ring 32 dwords x EW lanes | encode table
-// 256 x 16 B | input tile 16 rows x EW bytes. EW = 256: exactly 40 KiB, four
-// workgroups (16 waves) per CU.
+// a ring address wraps with one AND): ring ERS dwords x EW lanes (+ one guard
+// row, GD) | encode table 256 x 16 B (x TC copies at EW = 256) | input tile(s)
+// 16 rows x EW bytes. EW = 256 defaults: 16 + 1 + 4 x 16 + 4 KiB = 37 KiB,
+// four workgroups (16 waves) per CU.
 // IL: the batch's scratch layout (RansWork::il), a template parameter so that
 // the long-stream (contiguous) instance keeps its constant addressing.
 #ifndef ZR_ENC_TC256
 #define ZR_ENC_TC256 4
 #endif
+// DB: two input tiles written alternately (one barrier per tile) or one tile
+// (two barriers). ERS: output ring slots (dwords) per lane, flushed in bursts
+// of ERS / 2. GUARD: the guard row after the ring (see GD in enc_xn_body).
+// Round 6 (same box, 5 + 7 alternations, profiles/r06_enc_guard_ab.log): one
+// tile, a 16-slot ring and the guard row (37 KiB per workgroup, 4 per CU, four
+// table copies) against two tiles and no guard (40 KiB): encoder 0.1626 /
+// 0.1627 against 0.1649 / 0.1642 ms; one tile without the guard 0.1652 ms,
+// i.e. the second barrier per tile costs nothing measurable and the guard row
+// saves its two VALU per step pair. (Round 5 had measured the guard with
+// three table copies, to stay at 40 KiB with two tiles: 0.1653 against
+// 0.1595 ms, profiles/r05_ab23_guard.log.)
 #ifndef ZR_ENC_DB
-#define ZR_ENC_DB 1
+#define ZR_ENC_DB 0
+#endif
+#ifndef ZR_ENC_ERS
+#define ZR_ENC_ERS 16
+#endif
+#ifndef ZR_ENC_GUARD
+#define ZR_ENC_GUARD 1
 #endif
 #ifndef ZR_ENC_V2
 #define ZR_ENC_V2 1
@@ -674,19 +692,20 @@ __device__ __forceinline__ uint32_t enc_step_v2(uint32_t &X, const uint4 e, uint
 // LDS bytes of k_enc_xn's workgroup (ring | encode table | input tiles)
 template <uint32_t EW>
 constexpr uint32_t enc_xn_lds_bytes() {
-    return (ZR_ENC_DB != 0 ? 16u : 32u) * EW * 4 + 256u * 16 * (EW == 256 ? (uint32_t)ZR_ENC_TC256 : 1u) +
-           (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
+    return (uint32_t)ZR_ENC_ERS * EW * 4 + (ZR_ENC_GUARD != 0 && ZR_ENC_V2 != 0 && EW == 256 ? EW * 4 : 0u) +
+           256u * 16 * (EW == 256 ? (uint32_t)ZR_ENC_TC256 : 1u) + (ZR_ENC_DB != 0 ? 2u : 1u) * 16 * EW;
 }
 // the encoder of workgroup vblk (its blockIdx.x in k_enc_xn), LDS from the caller
 template <uint32_t EW, int ABL, bool IL>
 __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, const RansWork &w, uint32_t vblk,
                                             uint8_t *const lds) {
-    // DB: two input tiles, written alternately, so one barrier per tile
-    // separates a tile's writes from its reads (the other barrier kept the
-    // next tile's writes from overtaking slow readers); the room comes from a
-    // 16-slot ring flushed in 32-B bursts (pending <= 7 + 8 dwords)
+    // DB (off by default): two input tiles, written alternately, so one
+    // barrier per tile separates a tile's writes from its reads; with one
+    // tile a second barrier keeps the next tile's writes from overtaking slow
+    // readers (no measurable cost, profiles/r06_enc_guard_ab.log). The ring
+    // holds ERS = 16 slots flushed in 32-B bursts (pending <= 7 + 8 dwords).
     constexpr bool DB = ZR_ENC_DB != 0;
-    constexpr uint32_t ERS = DB ? 16 : 32;  // ring slots (dwords) per lane
+    constexpr uint32_t ERS = ZR_ENC_ERS;  // ring slots (dwords) per lane
     constexpr uint32_t FL = ERS / 2;        // dwords per flush burst
     constexpr uint32_t ETILE = 16;          // input rows (steps) per tile
     constexpr uint32_t RING_BYTES = ERS * EW * 4;  // a power of two
@@ -706,11 +725,17 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     // round trip on the wave: encoder 0.164 -> 0.173 ms, record encoder
     // 0.675 -> 0.688 ms. Dropped.)
     constexpr bool V2 = ZR_ENC_V2 != 0 && EW >= 256;
-    // (A guard row after the ring, so that a pair's overflow dword needs no
-    // wrap: 16 VALU fewer per tile, but it needs a 3-copy table to keep 4
-    // workgroups per CU, and 3 copies cost more than it saves: 0.1653 against
-    // 0.1595 ms, profiles/r05_ab23_guard.log. Removed.)
-    constexpr uint32_t RING_ALLOC = RING_BYTES;
+    // GD (ZR_ENC_GUARD, the 256-lane V2 shape): a guard row after the ring
+    // takes the overflow of a pair whose low dword is in the last row, so the
+    // overflow's address is the low one + ROW with no wrap (an immediate
+    // offset: two VALU fewer per step pair). Row 0's complete content is then
+    // its own ORs plus the guard: folded in (ds_or) when rows ERS/2.. are
+    // flushed, by which time the pair that crossed into row 0 has written the
+    // guard and the next crossing has not (<= 15 rows pending); row 0 is
+    // cleared when rows 0.. are flushed, its next writer being the ORs after
+    // the next wrap.
+    constexpr bool GD = ZR_ENC_GUARD != 0 && V2 && EW == 256;
+    constexpr uint32_t RING_ALLOC = RING_BYTES + (GD ? EW * 4 : 0u);
     static_assert(enc_xn_lds_bytes<EW>() == RING_ALLOC + 256 * 16 * TC + (DB ? 2 : 1) * ETILE * EW, "LDS layout");
     uint32_t *ring = reinterpret_cast<uint32_t *>(lds);
     uint4 *et = reinterpret_cast<uint4 *>(lds + RING_ALLOC);
@@ -879,7 +904,7 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
             asm("v_lshlrev_b32 %0, %1, %2\n\tv_and_or_b32 %0, %0, %3, %4"
                 : "=&v"(alo)
                 : "i"(__builtin_ctz(ROW) - 5), "v"(P), "s"((RING_BYTES - 1) & ~(ROW - 1)), "v"(tid * 4));
-            ahi = (alo + ROW) & (RING_BYTES - 1);
+            ahi = GD ? alo + ROW : (alo + ROW) & (RING_BYTES - 1);
             __hip_atomic_fetch_or(static_cast<uint32_t *>(__builtin_assume_aligned(lds + alo, 4)), (uint32_t)v, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_WORKGROUP);
             *reinterpret_cast<uint32_t *>(lds + ahi) = (uint32_t)(v >> 32);
@@ -916,6 +941,13 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
             const uint32_t *r = ring + (nfl & FL) * EW + tid;
 #pragma unroll
             for (int i = 0; i < (int)FL; i++) fd[i] = r[i * EW];
+            if constexpr (GD) {
+                static_assert(2 * FL == ERS, "GD: two flush halves");
+                if (nfl & FL)  // fold the guard into row 0 (the next wrap's ORs are there)
+                    __hip_atomic_fetch_or(ring + tid, ring[ERS * EW + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else  // row 0 read: cleared for the next wrap
+                    ring[tid] = 0u;
+            }
             fo = nfl >> 2;
             nfl += FL;
             flim += FL * 32;
@@ -979,6 +1011,7 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     v4u pend = issue_piece(ntiles - 1);
     build_table();
     if constexpr (V2O) ring[tid] = 0u;  // row 0: the first partial dword
+    if constexpr (GD) ring[ERS * EW + tid] = 0u;
     // FULL: every one of the 256 symbols has a frequency, so no coded symbol can
     // be missing from the table and the full tiles skip the check (two v_min3
     // per four steps; the check removed outright: encoder 0.1616 -> 0.1566 ms,
@@ -1087,6 +1120,14 @@ __device__ __forceinline__ void enc_xn_body(const uint8_t *raw, const KArgs &a, 
     // the partial dword (its nacc / 8 whole bytes count)
     const uint32_t nw = nw_of();
     auto rrow = [&](uint32_t d) -> uint32_t { return d & (ERS - 1); };
+    // GD: a row 0 pending after rows FL.. (the wrap not yet folded in by their
+    // flush) takes the guard; a row 0 pending first was folded at the flush
+    // before (or is the stream's first row), and the guard may already hold
+    // the next wrap's carry
+    if constexpr (GD) {
+        if ((nfl & (ERS - 1)) == FL && nw - nfl + ((P & 31) ? 1u : 0u) > FL)
+            __hip_atomic_fetch_or(ring + tid, ring[ERS * EW + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     {
         const uint32_t *r = ring + tid;
         while (nw - nfl >= 4) {
