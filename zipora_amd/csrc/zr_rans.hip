@@ -3005,7 +3005,13 @@ __global__ __launch_bounds__(X1W) void k_dec_x1_ring(const uint8_t *enc, uint8_t
 //     reads outran its ring decodes again with x1_dec_generic.
 // ----------------------------------------------------------------------
 constexpr uint32_t XF = 1024;  // records per workgroup
-constexpr uint32_t XG = 8;     // tiles per output group (16 * XG bytes per lane per store run)
+#ifndef ZR_X1_XG
+#define ZR_X1_XG 8
+#endif
+#ifndef ZR_X1_PAIR
+#define ZR_X1_PAIR 0
+#endif
+constexpr uint32_t XG = ZR_X1_XG;  // 16-step tiles per output group (16 * XG bytes per lane per store run)
 constexpr uint32_t NSET = 1;   // staging register sets: a refill lands NSET boundaries after its loads
 #ifndef ZR_X1_T32
 #define ZR_X1_T32 1  // 32-step tiles with the predicted-consumption refill rule
@@ -3225,27 +3231,56 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
         constexpr uint32_t TT = 32, TPG = 16 * XG / TT;
         const uint32_t nt32 = (cmax + TT - 1) / TT;
         uint32_t ppos8 = pos8 + TT * 8;  // pos8 at the previous boundary (first: one byte a step)
+        bool hasB = false;  // PAIR: f holds the segment below e's, loaded, not yet landed
         auto boundary32 = [&](uint32_t t, auto wc) __attribute__((always_inline)) {
             // every read of tile t - 1 (lanes live in it) was at or above pos - 4
             bad |= fast && TT * t < nn + TT && (int32_t)(pos8 - 32 - ((uint32_t)lo64 << 3)) < 0;
             if (t >= 1) {
-                asm volatile("s_waitcnt vmcnt(%4)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3) : "i"(decltype(wc)::value) : "memory");
+                if constexpr (ZR_X1_PAIR != 0)
+                    asm volatile("s_waitcnt vmcnt(%8)"
+                                 : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3)
+                                 : "i"(decltype(wc)::value)
+                                 : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3) : "i"(decltype(wc)::value) : "memory");
                 const bool landable = (int32_t)(pos8 - ((uint32_t)lo64 << 3)) <= 64 * 8;
-                if (pnd && landable) {
+                const bool lE = pnd && landable, lO = ZR_X1_PAIR && !pnd && hasB && landable;
+                if (lE) {
                     lo64 -= 64;
                     put_seg((uint32_t)lo64, e0, e1, e2, e3);
                 }
+                if (lO) {
+                    lo64 -= 64;
+                    put_seg((uint32_t)lo64, f0, f1, f2, f3);
+                }
                 pnd = pnd && !landable;
+                hasB = hasB && !lO;
             }
             const uint32_t used8 = ppos8 - pos8;
             ppos8 = pos8;
             const bool need = fast && TT * t < nn && (int32_t)(pos8 - used8 - ((uint32_t)lo64 << 3)) <= 64 * 8;
-            const bool issue = pnd || need;  // (a segment that did not land: fetched again)
+            // (a segment that did not land: fetched again; a lane whose f set
+            // holds the next segment issues nothing new)
+            const bool issue = pnd || (need && !hasB);
             const uintptr_t ga = issue ? clampa(lo64 - 64) : dummy;
             asm_load16(e0, ga);
             asm_load16_off<16>(e1, ga);
             asm_load16_off<32>(e2, ga);
             asm_load16_off<48>(e3, ga);
+            if constexpr (ZR_X1_PAIR != 0) {
+                // PAIR: a fresh segment that is a 128-B line's upper half brings
+                // the lower half along into f (landing a boundary or more later
+                // from registers), so no line is fetched twice
+                const bool pair = issue && !pnd && !hasB && (lo64 & 127) == 0 && lo64 - 128 >= lo_lim;
+                if (pair) {  // (tied operands: the phi at the merge keeps f in place)
+                    const uintptr_t gb = lo64 - 128;
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(f0) : "v"(gb) : "memory");
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "+v"(f1) : "v"(gb) : "memory");
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "+v"(f2) : "v"(gb) : "memory");
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:48" : "+v"(f3) : "v"(gb) : "memory");
+                }
+                hasB = hasB || pair;
+            }
             pnd = issue;
         };
         auto tile32 = [&](uint32_t t, uint32_t *o, auto irr) __attribute__((always_inline)) {
@@ -3277,7 +3312,11 @@ __global__ __launch_bounds__(XF) void k_dec_x1_fast(const uint8_t *enc, uint8_t 
         using W0 = std::integral_constant<int, 0>;
         using WX = std::integral_constant<int, XG>;
         auto resync = [&]() __attribute__((always_inline)) {
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
+            if constexpr (ZR_X1_PAIR != 0)
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1), "+v"(f2),
+                             "+v"(f3)::"memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3)::"memory");
         };
         auto group32 = [&](uint32_t g, auto irr) __attribute__((always_inline)) {
             constexpr bool IRR = decltype(irr)::value;
