@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--groups", type=int, default=1,
                    help="rans: code the buffers as G groups on G HIP streams after the shared table "
                         "(encode+compaction+decode of one group overlap the others')")
+    p.add_argument("--graph", type=int, default=0,
+                   help="rANS workload, one rank: untimed steps replay a HIP graph of the step "
+                        "(the event-timed steps run eagerly)")
     p.add_argument("--pipeline", action="store_true",
                    help="rans: two distinct batches alternate; each step codes one (encode -> decode on the "
                         "main stream) while the histogram + table of the next one run on a second stream")
@@ -372,17 +375,17 @@ def _measure(torch, dist, world, dev, L, fn, args, names, also=()):
     kms = {}
     if select is None:  # (an older library in an A/B run: every kernel timed at once)
         L.zr_timer_reset()
-        L.zr_timer_enable(1)
+        _timer_enable(L, 1)
         for _ in range(max(1, min(args.steps, 10))):
             fn()
         torch.cuda.synchronize(dev)
-        L.zr_timer_enable(0)
+        _timer_enable(L, 0)
         kms = {k: round(kernel_ms(L, k)[0], 4) for k in names}
         dominant = max(names, key=lambda k: kms[k])
         L.zr_timer_reset()
-        L.zr_timer_enable(1)
+        _timer_enable(L, 1)
         dt = _timed(torch, dist, world, dev, fn, args.steps, 0)
-        L.zr_timer_enable(0)
+        _timer_enable(L, 0)
         tms = {k: kernel_ms(L, k)[0] for k in [dominant, *also]}
         return dt, dominant, tms[dominant], kms, tms
     # one kernel timed per pass, on every TIME_EVERY-th step: timed all at once
@@ -392,10 +395,10 @@ def _measure(torch, dist, world, dev, L, fn, args, names, also=()):
         L.zr_timer_reset()
         select(k.encode())
         for i in range(2 * TIME_EVERY):
-            L.zr_timer_enable(1 if i % TIME_EVERY == 0 else 0)
+            _timer_enable(L, 1 if i % TIME_EVERY == 0 else 0)
             fn()
         torch.cuda.synchronize(dev)
-        L.zr_timer_enable(0)
+        _timer_enable(L, 0)
         kms[k] = round(kernel_ms(L, k)[0], 4)
     dominant = max(names, key=lambda k: kms[k])
     timed = [dominant] + [k for k in also if k != dominant]
@@ -408,10 +411,10 @@ def _measure(torch, dist, world, dev, L, fn, args, names, also=()):
         on = i % TIME_EVERY == 0
         if on:
             select(timed[(i // TIME_EVERY) % len(timed)].encode())
-        L.zr_timer_enable(1 if on else 0)
+        _timer_enable(L, 1 if on else 0)
 
     dt = _timed(torch, dist, world, dev, fn, args.steps, 0, timer=timer)
-    L.zr_timer_enable(0)
+    _timer_enable(L, 0)
     tms = {}
     for k in timed:  # (a kernel no timed step reached keeps its instrumented-pass time)
         ms, cnt = kernel_ms(L, k)
@@ -425,6 +428,13 @@ def _measure(torch, dist, world, dev, L, fn, args, names, also=()):
 
 
 TIME_EVERY = 4
+_TIMER_ON = False  # a step runs with the library's kernel timer on (graph mode: eagerly)
+
+
+def _timer_enable(L, on):
+    global _TIMER_ON
+    _TIMER_ON = bool(on)
+    L.zr_timer_enable(1 if on else 0)
 
 
 def _timed(torch, dist, world, dev, fn, steps, warmup, timer=None):
@@ -790,13 +800,46 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
 
     step()
     torch.cuda.synchronize(dev)
+    fn = step
+    graph = bool(getattr(args, "graph", 0)) and not pipe and G == 1 and comm is None
+    if graph:
+        # the whole step (histogram + table, encode with its compaction, the
+        # decode's status clear and decode) captured once; untimed steps replay
+        # it on the same stream, the event-timed ones run eagerly (a graph
+        # bakes in the timer state it was captured with)
+        cap = torch.cuda.Stream(dev)
+        cap.wait_stream(stream)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            cs = torch.cuda.current_stream(dev)
+            if fused:
+                bt.table_from_data(raw, cs)
+            else:
+                bt.histogram(raw, cs, zeroed=consume)
+                bt.tables_from_hist(cs, consume=consume)
+            bt.encode(raw, enc, cs)
+            bt.decode(enc, out, cs)
+        torch.cuda.synchronize(dev)
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize(dev)
+        if not diag:
+            bt.raise_on_error()
+            if not torch.equal(out, raw):
+                raise SystemExit("decode mismatch after the first graph replay")
+
+        def fn():
+            if _TIMER_ON:
+                step()
+            else:
+                g.replay()
     if not diag:
         b_, r_ = last_raw()
         b_.raise_on_error()
         if not torch.equal(out, r_):
             raise SystemExit("decode mismatch after the first step")
 
-    dt, dom, dom_ms, kms, tms = _measure(torch, dist, world, dev, L, step, args,
+    dt, dom, dom_ms, kms, tms = _measure(torch, dist, world, dev, L, fn, args,
                                          ["rans_encode", "rans_decode", "rans_compact", "histogram"],
                                          also=["rans_decode"])
     if not diag:
@@ -825,7 +868,7 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
         comm.close()
     if diag:  # tools/*.sh read the kernel times; no metric from a diagnostic build
         return {"diagnostic": diag, "kernels_ms": kms, "ms_per_step": round(dt / args.steps * 1e3, 4),
-                "timed_ms": {k: round(v, 4) for k, v in tms.items()}}
+                "timed_ms": {k: round(v, 4) for k, v in tms.items()}, "graph": graph}
     single = B == 1
     literal = single and N == 4096
     wl = "rans_literal" if literal else f"rans_n2e{N.bit_length() - 1}" if single else "rans"
@@ -875,6 +918,7 @@ def run_rans(args, torch, dist, world, rank, dev, zr, L, B, n, N, diag=(), host=
         "ratio": round(comp_bytes / total, 5),
     }
     res.update(exch)
+    res["step_graph"] = graph  # untimed steps replayed a HIP graph of the step
     if rank == 0 and world == 1 and host_path and not args.no_host_path:
         res.update(host_pipe_rates(zr, bt, host[:total], [n] * B, N, args.steps))
     if rank == 0 and world == 1 and cpu and not args.no_cpu_baseline:

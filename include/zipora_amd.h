@@ -25,12 +25,13 @@
  * HIP stream (hipStream_t passed as void*, NULL = default stream) and report
  * per-buffer status into a device int32 array; read it after synchronising.
  * Graph capture: zr_rans_encode/decode_batch_dev, zr_histogram_dev,
- * zr_rans_dtab_from_hist*_dev and the RCCL calls may be captured into a HIP
- * graph and replayed (they keep no host-side state). Every other _dev call returns
- * ZR_UNSUPPORTED on a capturing stream: zr_rans_dtab_upload and
- * zr_huff_decode_dev stage host data through memory a host callback frees,
- * zr_rans_dtab_from_data_dev picks its ticket counters by a host counter, and
- * zr_huff_encode_dev, zr_fse_compress_dev, zr_fse_decompress_dev,
+ * zr_rans_dtab_from_hist*_dev, zr_rans_dtab_from_data_dev and the RCCL calls
+ * may be captured into a HIP graph and replayed (they keep no host-side state;
+ * zr_rans_dtab_from_data_dev keeps the ticket slot it was captured with, so
+ * replays of one such graph must not run concurrently with each other). Every
+ * other _dev call returns ZR_UNSUPPORTED on a capturing stream:
+ * zr_rans_dtab_upload and zr_huff_decode_dev stage host data through memory a
+ * host callback frees, and zr_huff_encode_dev, zr_fse_compress_dev, zr_fse_decompress_dev,
  * zr_ctx_huff_encode_dev, zr_ctx_huff_decode_dev and the
  * zr_rans_compressor_*_batch_dev calls are not capture-validated.
  */
@@ -159,13 +160,15 @@ int32_t zr_rans_dtab_from_hist_consume_dev(uint32_t *hist_dev, uint32_t n_tables
  * table (Rans64Encoder::new, rans.rs:208-235) into dtab_dev (one table). The
  * RansBlobStore::train / RansCompressor::new path of a single GPU
  * (blob_store/entropy.rs:212-222, compression/mod.rs:433-450). hist_dev: 256
- * u32, all zero on entry, left all zero (the counts are consumed). Not on a
- * capturing stream (ZR_UNSUPPORTED): each call picks its workgroups' ticket
- * counters by a host-side call counter, slot (call number % 64). Limit: fewer
- * than 64 calls of this function may be executing at once in the process
- * (calls queued on one stream run one after another and never share a slot;
- * 64 or more concurrent streams each running one could pair two calls on a
- * slot, and a table would then be built before its histogram is complete). */
+ * u32, all zero on entry, left all zero (the counts are consumed). Each call
+ * picks its workgroups' ticket counters by a host-side call counter, slot
+ * (call number % 64). Limit: fewer than 64 calls of this function may be
+ * executing at once in the process (calls queued on one stream run one after
+ * another and never share a slot; 64 or more concurrent streams each running
+ * one could pair two calls on a slot, and a table would then be built before
+ * its histogram is complete). Capturable: a captured call keeps its slot in
+ * every replay, so replays of one graph must not overlap each other (replays
+ * on one stream never do). */
 int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *batch, uint32_t *hist_dev,
                                    void *dtab_dev, void *stream);
 /* The name of the xN decode kernel a batch of n_buffers x n_streams (every

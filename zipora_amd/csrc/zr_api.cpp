@@ -515,7 +515,8 @@ int32_t zr_release_call_contexts(void) {
 }
 int32_t zr_memset_dev(void *dst, int value, size_t bytes, void *stream) {
     ZR_GUARD_BEGIN
-    ZR_HIP(hipMemsetAsync(dst, value, bytes, (hipStream_t)stream));
+    fill_dev(dst, value, bytes, (hipStream_t)stream);  // (a kernel: graph-capturable, see fill_dev)
+    ZR_HIP(hipGetLastError());
     return ZR_OK;
     ZR_GUARD_END
 }

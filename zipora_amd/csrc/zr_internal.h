@@ -21,6 +21,13 @@ inline bool capturing(hipStream_t s) {
     return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 void clear_error();
+// fill `bytes` bytes at device address p with the byte `value`, stream-ordered,
+// by a kernel (zr_rans.hip): the memsets of the capturable calls. A
+// hipMemsetAsync of 64 B or more captured into a HIP graph writes other data
+// (address-like words) on the graph's second and later replays on this ROCm
+// (tools/graph_memset_probe.py, profiles/r06_graph_memset_probe.log); a kernel
+// node replays as captured.
+void fill_dev(void *p, int value, size_t bytes, hipStream_t s);
 
 #define ZR_HIP(expr)                                                                       \
     do {                                                                                   \

@@ -22,6 +22,26 @@
 namespace zr {
 
 // ------------------------------------------------------------------ helpers
+// byte fill (fill_dev, zr_internal.h): head bytes to 16-B alignment, 16-B
+// stores grid-stride, tail bytes
+__global__ __launch_bounds__(256) void k_fill(uint8_t *p, uint32_t v, uint64_t n) {
+    const uint64_t head = min<uint64_t>(n, (16 - (((uintptr_t)p) & 15)) & 15);
+    const uint64_t nv = (n - head) / 16, tail0 = head + nv * 16;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    if (t < head) p[t] = (uint8_t)v;
+    if (t < n - tail0) p[tail0 + t] = (uint8_t)v;
+    uint4 *q = reinterpret_cast<uint4 *>(p + head);
+    const uint4 w = make_uint4(v, v, v, v);
+    for (uint64_t i = t; i < nv; i += stride) q[i] = w;
+}
+void fill_dev(void *p, int value, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    const uint32_t v = (uint32_t)(uint8_t)value * 0x01010101u;
+    const uint64_t blocks = (bytes / 16 + 255) / 256;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(blocks, 1), 4096);
+    hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, s, reinterpret_cast<uint8_t *>(p), v, (uint64_t)bytes);
+}
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
 // the lane-interleaved xN scratch (RansWork::il): the IL_SPAN streams of a group
@@ -1787,7 +1807,7 @@ constexpr int DT2 = 16;  // steps per tile
 // every workgroup reads all N stream lengths of its buffer for its own offset
 // and the buffer's checks. fused == 0: k_dec_hdr (and k_scan) ran first.
 // Status protocol (both modes): the host clears status[b] of the batch to
-// ZR_OK (one stream-ordered memset of 4 B per buffer) before the first decode
+// ZR_OK (one stream-ordered fill of 4 B per buffer, k_fill) before the first decode
 // kernel, and a workgroup or lane that finds an error stores ZR_INVALID_INPUT
 // (rans.rs:480-482, :563-568, :601-610); stores of the same value race
 // harmlessly. So no status depends on what the workspace held before the call,
@@ -3675,8 +3695,8 @@ int32_t zr_rans_dtab_from_data_dev(const uint8_t *raw, const zr_rans_batch *bt, 
     ZR_GUARD_BEGIN
     clear_error();
     if (!bt || !hist_dev || !dtab_dev) return set_error(ZR_INVALID_INPUT, "null argument");
-    if (capturing((hipStream_t)stream))  // the per-call tag comes from a host counter
-        return set_error(ZR_UNSUPPORTED, "zr_rans_dtab_from_data_dev on a capturing stream");
+    // (captured into a graph, the call keeps the ticket slot it was captured
+    // with: replays of one graph must not overlap each other, see the header)
     KArgs a = kargs(bt);
     const uint64_t chunk = 64 * 1024;
     const uint32_t nchunk = bt->max_len ? (uint32_t)ceil_div(bt->max_len, chunk) : 1u;
@@ -3741,7 +3761,7 @@ int32_t zr_rans_encode_batch_dev(const zr_rans_batch *bt, const uint8_t *raw, ui
     if (bt->max_len >= a.N && a.N > 1) {
         const bool narrow = narrow_batch(a);
         if (narrow) {  // the narrow encoder adds wave sums into the block sums
-            ZR_HIP(hipMemsetAsync(w.blocksum, 0, sizeof(uint64_t) * gx, s));
+            fill_dev(w.blocksum, 0, sizeof(uint64_t) * gx, s);
             launch_timed("rans_encode", w.il ? k_enc_xn<64, 0, true> : k_enc_xn<64, 0, false>,
                          dim3((uint32_t)round_up(ceil_div(a.N, 64) * a.B, 16)), dim3(64), 0, s, raw, a, w);
         } else {
@@ -3822,9 +3842,10 @@ int32_t zr_rans_decode_batch_dev(const zr_rans_batch *bt, const uint8_t *enc, ui
     if (bt->max_len >= a.N && a.N > 1) {
         // every status starts at ZR_OK and the xN kernels only ever store
         // ZR_INVALID_INPUT (see dec_xn_body); the x1 decoders below write the
-        // statuses of the x1 buffers themselves. 4 B per buffer, stream-ordered,
+        // statuses of the x1 buffers themselves. 4 B per buffer, stream-ordered
+        // (k_fill, not hipMemsetAsync: see fill_dev),
         // capture-safe; no status depends on the workspace's earlier content
-        ZR_HIP(hipMemsetAsync(bt->status, 0, sizeof(int32_t) * a.B, s));
+        fill_dev(bt->status, 0, sizeof(int32_t) * a.B, s);
         // more than SCAN_FUSE blocks per buffer: the block sums and their scan
         // first; otherwise every decoder workgroup reads its buffer's stream
         // lengths itself (fused)
