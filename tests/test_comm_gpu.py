@@ -63,3 +63,56 @@ def test_comm_rejects_bad_rank():
     from zipora_amd import dist as zd
     with pytest.raises(zr.ZiporaError):
         zd.RcclComm(2, 5, unique_id=bytes(128))
+
+
+def test_rccl_allreduce_captured_step_replays():
+    """The header's claim that the RCCL calls may be captured: the shared-table
+    step of the multi-GPU bench (histogram, in-place u32 all-reduce on a
+    world-1 communicator, consuming table build, encode, decode) captured into
+    a HIP graph and replayed three times, each replay equal to the oracle."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import oracle_ffi as O
+    from zipora_amd import dist as zd
+    from zipora_amd.device import RansDeviceBatch
+    comm = zd.RcclComm(1, 0)
+    try:
+        lens = [4096 * 30 + 7, 4096 * 30]
+        bt = RansDeviceBatch(lens, 4096, shared_table=True)
+        raw = bt.new_raw()
+        enc, out = bt.new_enc(), bt.new_raw()
+        side = torch.cuda.Stream()
+
+        def step(s):
+            bt.histogram(raw, s, zeroed=True)
+            comm.allreduce_histogram(bt.hist, s.cuda_stream)
+            bt.tables_from_hist(s, consume=True)
+            bt.encode(raw, enc, s)
+            bt.decode(enc, out, s)
+
+        def load(seed, kind):
+            ds = [zr.synth(kind, n, seed=seed + i) for i, n in enumerate(lens)]
+            for b, d in enumerate(ds):
+                o = bt.raw_off_host[b]
+                raw[o:o + len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+            return ds
+
+        load(1, "t")
+        with torch.cuda.stream(side):
+            step(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            step(torch.cuda.current_stream())
+        for seed, kind in ((1, "t"), (2, "z"), (3, "u")):
+            ds = load(seed, kind)
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            bt.raise_on_error()
+            tab = O.rans_table(O.histogram(b"".join(ds)))
+            for b, d in enumerate(ds):
+                assert bt.raw_of(out, b) == d
+                assert bt.encoded(enc, b) == O.rans_encode(tab, 4096, d)
+    finally:
+        comm.close()
